@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: cell-updates/s of the weather-sim time step on MI355X (BASELINE.json metric).
+
+Default workload (BASELINE configs[1], "C2"): Shallow Water 4096 x 4096, fp64, RK4 (the
+reference's default integrator, weather_sim.hpp:159), jet_stream initial condition,
+inputs resident in HBM. One "step" = one full time step of the whole grid, all N ranks.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5] [--method rk4|rk2|euler]
+
+N > 1 (launched by torch.distributed.run, one process per GPU): the same global grid is
+y-slab decomposed over the ranks (strong scaling) and halo rows move over RCCL inside
+libws_hip.so. Timing: barrier + torch.cuda.synchronize() on both sides of exactly K steps,
+max over ranks. value = W*H*L*K / that time (whole job).
+
+The JSON line also carries:
+  roofline     dominant stage kernel: algorithmic bytes per launch / mean launch time
+               (HIP events on the kernel's stream inside the timed region) vs 8 TB/s;
+               traffic from profiles/traffic_<config>.json (rocprofv3 PMC) when present.
+  cpu_baseline the reference CPU solver (oracle/_ref, compiled from /root/reference
+               sources) or, if absent, the C oracle port, timed on host cores on a bounded
+               sample of the same workload (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nvidia-jetson-workload_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "cell-updates/sec + achieved HBM GB/s, SWE 4096^2 at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "c2": dict(W=4096, H=4096, L=1, model=0, fp64=True, ic="jet_stream",
+               workload="C2: Shallow Water 4096x4096 fp64, 1 level"),
+    "c3": dict(W=2048, H=2048, L=1, model=1, fp64=False, ic="zonal_flow",
+               workload="C3: Barotropic (reference semantics: SWE tendencies, RK4->RK2) 2048x2048 fp32"),
+    "c4": dict(W=1024, H=1024, L=32, model=2, fp64=False, ic="jet_stream",
+               workload="C4: Primitive Equations (reference semantics) 1024x1024x32 levels fp32"),
+    "c5": dict(W=16384, H=16384, L=1, model=0, fp64=True, ic="jet_stream",
+               workload="C5: Shallow Water 16384x16384 fp64"),
+}
+METHODS = {"euler": 0, "rk2": 1, "rk4": 2}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(conf, method, budget_s=20.0):
+    """Time the reference CPU solver (or the oracle port) on a bounded sample."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    variant = "f64" if conf["fp64"] else "f32"
+    ref = os.path.join(ROOT, "oracle", "_ref", f"ws_ref_{variant}")
+    W, H = conf["W"], conf["H"] * conf["L"]  # levels stacked (the reference is 2-D only)
+    if conf["H"] * conf["W"] * conf["L"] > 4096 * 4096 * 2:
+        W, H = 4096, 4096  # C5 does not fit host memory in the reference layout: same per-cell work
+    # pilot: 1 step to size the sample to ~budget_s
+    def run_ref(steps):
+        spec = "\n".join([f"cfg width {W}", f"cfg height {H}", f"cfg model {conf['model']}",
+                          f"cfg method {method}", "cfg max_time 1e30", "create", f"ic {conf['ic']}",
+                          "initialize", "time_run 1", f"time_run {steps}"]) + "\n"
+        with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+            f.write(spec)
+        try:
+            out = subprocess.run([ref, f.name], env=env, capture_output=True, text=True, timeout=600).stdout
+        finally:
+            os.unlink(f.name)
+        secs = [float(l.split()[2]) for l in out.splitlines() if l.startswith("TIME_RUN")]
+        return secs[-1]
+
+    if os.path.exists(ref):
+        pilot = run_ref(1)
+        steps = max(1, min(200, int(budget_s / max(pilot, 1e-6))))
+        secs = run_ref(steps)
+        kind = "reference"
+        what = f"reference weather_simulation.cpp (oracle/_ref/ws_ref_{variant}, -O3 -fopenmp)"
+    else:
+        from oracle.ws_oracle import OracleSim
+        import numpy as np
+        sim = OracleSim(W, H, conf["model"], method, max_time=1e30, precision=variant)
+        sim.initialize()
+        t0 = time.perf_counter()
+        sim.step()
+        pilot = time.perf_counter() - t0
+        steps = max(1, min(200, int(budget_s / max(pilot, 1e-6))))
+        t0 = time.perf_counter()
+        sim.run(steps)
+        secs = time.perf_counter() - t0
+        kind = "port"
+        what = "C oracle port (oracle/ws_oracle.c, -O3 -fopenmp)"
+    return {"value": W * H * steps / secs, "unit": "cell-updates/s", "cores": threads, "kind": kind,
+            "sample": f"{what}: {W}x{H}, {steps} steps after 1 warm-up step, {secs:.2f} s wall, "
+                      f"OMP_NUM_THREADS={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--method", default="rk4", choices=sorted(METHODS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    os.environ.setdefault("WS_QUIET", "1")
+    import torch  # plumbing: contract timing (barrier + torch.cuda.synchronize); loaded before libws_hip
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("gloo")  # bootstrap (RCCL unique id) + host-side max over ranks
+
+    import weather_sim as ws
+    from weather_sim import _native
+
+    conf = CONFIGS[args.config]
+    method = METHODS[args.method]
+    cfg = ws.SimulationConfig()
+    cfg.grid_width, cfg.grid_height, cfg.num_levels = conf["W"], conf["H"], conf["L"]
+    cfg.model = conf["model"]
+    cfg.integration_method = method
+    cfg.double_precision = conf["fp64"]
+    cfg.device_id = local
+    cfg.max_time = 1e30  # run() would otherwise stop at t >= 10 (1000 steps of dt = 0.01)
+
+    if world > 1:
+        import ctypes
+        uid = torch.zeros(_native.COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            buf = (ctypes.c_uint8 * _native.COMM_ID_BYTES)()
+            _native.check(_native.lib.ws_comm_get_unique_id(buf))
+            uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        dist.broadcast(uid, 0)
+        sim = ws.WeatherSimulation(cfg, _slab=(rank, world, bytes(uid.tolist())))
+    else:
+        sim = ws.WeatherSimulation(cfg)
+
+    ic = {"jet_stream": ws.JetStreamInitialCondition, "zonal_flow": ws.ZonalFlowInitialCondition}[conf["ic"]]()
+    sim.set_initial_condition(ic)
+    sim.initialize()  # on a slab, the IC is evaluated in global coordinates for the owned rows
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if args.warmup > 0:
+        sim.run(args.warmup)
+    sim.set_kernel_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    taken = sim.run(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    assert taken == args.steps, (taken, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+
+    cells = conf["W"] * conf["H"] * conf["L"]
+    value = cells * args.steps / elapsed
+    stats = sim.kernel_timing()
+    dev_ms, launches = sim.last_run_stats()
+    # dominant kernel = largest total device time
+    kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
+    achieved = bpl / (tot_ms / n * 1e-3) / 1e9
+    step_bytes = sum(b for (_, _, b) in stats.values())
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get(f"kind{kind}")
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if conf["fp64"] else "f32",
+        "data": "synthetic (reference jet_stream/zonal_flow initial condition), inputs resident in HBM",
+        "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [conf["W"], conf["H"]],
+                   "levels": conf["L"], "integrator": args.method,
+                   "parallelism": f"y-slab x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": f"stage{kind}", "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n},
+        "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
+        "kernel_stats": {f"stage{k}": {"launches": v[0], "mean_ms": v[1] / v[0], "bytes": v[2],
+                                       "gbs": v[2] / (v[1] / v[0] * 1e-3) / 1e9} for k, v in stats.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(conf, method)
+        except Exception as e:  # the GPU number stands on its own
+            log(f"cpu baseline failed: {e!r}")
+            result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,236 @@
+/* ws_hip.h -- C ABI of the MI355X-native weather-sim time-step library (libws_hip.so).
+ *
+ * This is the drop-in boundary for the reference's weather-sim hot path
+ * (/root/reference/src/weather-sim). Every entry point is `extern "C"`, takes plain
+ * pointers / sizes, returns an int status (WS_OK == 0) and never throws; the message of
+ * the last failure on the calling thread is available from ws_last_error(). No torch or
+ * C++ types cross the boundary. All compute runs as hand-written HIP kernels on gfx950;
+ * there is no CPU fallback: without a HIP device every creating call fails with
+ * WS_ERR_DEVICE.
+ *
+ * Reference interfaces replaced (paths relative to src/weather-sim/cpp):
+ *   ws_config_t                   SimulationConfig           include/weather_sim/weather_sim.hpp:155-191
+ *   ws_metrics_t                  PerformanceMetrics         include/weather_sim/weather_sim.hpp:196-223
+ *   ws_grid_*                     WeatherGrid                include/weather_sim/weather_sim.hpp:254-412,
+ *                                                            src/weather_grid.cpp:15-142, and the pybind
+ *                                                            field copies src/python_bindings.cpp:22-114,240-284
+ *   ws_grid_apply_initial_condition  InitialCondition::initialize  src/initial_conditions.cpp:48-608
+ *   ws_sim_*                      WeatherSimulation          include/weather_sim/weather_sim.hpp:417-544,
+ *                                                            src/weather_simulation.cpp:17-158
+ *   ws_adapter_*                  KernelAdapter (plugin API) include/weather_sim/gpu_adaptability.hpp:242-329
+ *   ws_launch_shallow_water_kernel   launchShallowWaterKernel   src/kernels/shallow_water_kernels.cu:704-719
+ *   ws_launch_diagnostics_kernels    launchDiagnosticsKernels   src/kernels/shallow_water_kernels.cu:830-840
+ *   ws_device_info / ws_is_available AdaptiveKernelManager::getDeviceCapabilities / isCudaAvailable
+ *                                                            include/weather_sim/gpu_adaptability.hpp:128-237
+ *   ws_comm_* / ws_sim_create_slab   (new: the reference has no distributed path)
+ */
+#ifndef WS_HIP_H
+#define WS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WS_ABI_VERSION 1
+
+/* status codes */
+enum {
+    WS_OK = 0,
+    WS_ERR_INVALID = 1,     /* bad argument (reference: std::invalid_argument -> ValueError) */
+    WS_ERR_DEVICE = 2,      /* HIP runtime / no device (reference: CUDA_CHECK -> false) */
+    WS_ERR_SHAPE = 3,       /* array shape mismatch (reference setters: std::runtime_error) */
+    WS_ERR_UNSUPPORTED = 4,
+    WS_ERR_COMM = 5         /* RCCL failure */
+};
+
+/* field ids (WeatherGrid members, weather_sim.hpp:403-411) */
+enum {
+    WS_FIELD_U = 0, WS_FIELD_V = 1, WS_FIELD_H = 2, WS_FIELD_P = 3,
+    WS_FIELD_T = 4, WS_FIELD_Q = 5, WS_FIELD_VORTICITY = 6, WS_FIELD_DIVERGENCE = 7
+};
+
+/* element types */
+enum { WS_F32 = 0, WS_F64 = 1 };
+
+/* enum values identical to weather_sim.hpp:30-76 */
+enum { WS_MODEL_SHALLOW_WATER = 0, WS_MODEL_BAROTROPIC = 1, WS_MODEL_PRIMITIVE_EQUATIONS = 2, WS_MODEL_GENERAL = 3 };
+enum { WS_EULER = 0, WS_RK2 = 1, WS_RK4 = 2, WS_ADAMS_BASHFORTH = 3, WS_SEMI_IMPLICIT = 4 };
+enum { WS_BACKEND_CUDA = 0, WS_BACKEND_CPU = 1, WS_BACKEND_HYBRID = 2, WS_BACKEND_ADAPTIVE_HYBRID = 3 };
+
+/* SimulationConfig (weather_sim.hpp:155-191). Scalars are passed as double and rounded to
+ * the simulation precision (fp32 unless double_precision != 0) exactly as the reference
+ * stores them in scalar_t. output_path stays on the host side of the boundary. */
+typedef struct ws_config {
+    int32_t model;
+    int32_t grid_type;
+    int32_t integration_method;
+    int32_t boundary_condition;
+    int32_t grid_width;
+    int32_t grid_height;
+    int32_t num_levels;          /* >1: L independent 2-D levels, fields are [L][H][W] */
+    double dx, dy, dt;
+    double gravity, coriolis_f, beta, viscosity, diffusivity;
+    int32_t compute_backend;
+    int32_t double_precision;    /* honoured: 0 -> fp32 (bitwise = reference), 1 -> fp64 */
+    int32_t device_id;
+    int32_t num_threads;
+    double max_time;
+    int32_t max_steps;
+    int32_t output_interval;
+    uint32_t random_seed;
+} ws_config_t;
+
+/* PerformanceMetrics (weather_sim.hpp:196-223). Times are device-event milliseconds
+ * (not integer-truncated). */
+typedef struct ws_metrics {
+    double total_time_ms;
+    double compute_time_ms;
+    double memory_transfer_time_ms;
+    double io_time_ms;
+    int32_t num_steps;
+} ws_metrics_t;
+
+/* DeviceCapabilities (gpu_adaptability.hpp:35-88), filled for the HIP device */
+typedef struct ws_device_info {
+    char device_name[256];
+    char arch[64];               /* e.g. "gfx950" */
+    int32_t compute_capability_major, compute_capability_minor;
+    int32_t multiprocessors;     /* CUs */
+    int32_t cuda_cores;          /* stream processors = CUs * 64 */
+    int64_t global_memory;       /* bytes */
+    int32_t shared_memory_per_block;
+    int32_t max_threads_per_block;
+    int32_t max_threads_per_multiprocessor;
+    int32_t clock_rate_khz;
+    int32_t memory_clock_rate_khz;
+    int32_t memory_bus_width;
+    int32_t wavefront_size;
+} ws_device_info_t;
+
+typedef struct ws_grid ws_grid_t;
+typedef struct ws_sim ws_sim_t;
+
+const char* ws_last_error(void);
+int ws_abi_version(void);
+int ws_is_available(int32_t* available);
+int ws_device_count(int32_t* count);
+int ws_device_info(int32_t device, ws_device_info_t* out);
+void ws_config_default(ws_config_t* cfg);
+
+/* ---- WeatherGrid ---------------------------------------------------------------- */
+int ws_grid_create(int32_t width, int32_t height, int32_t num_levels, int32_t dtype, int32_t device,
+                   ws_grid_t** out);
+int ws_grid_destroy(ws_grid_t* grid);
+int ws_grid_reset(ws_grid_t* grid);
+int ws_grid_get_dims(const ws_grid_t* grid, int32_t* width, int32_t* height, int32_t* num_levels,
+                     int32_t* dtype);
+int ws_grid_set_spacing(ws_grid_t* grid, double dx, double dy);
+int ws_grid_get_spacing(const ws_grid_t* grid, double* dx, double* dy);
+/* Copy a (height, width) C-contiguous host array of `dtype` into / out of one level of a
+ * field (level = -1: all levels, host array (num_levels, height, width)). A dtype
+ * different from the grid's is converted like a C cast. Reading VORTICITY/DIVERGENCE
+ * first materialises pending diagnostics (see ws_grid_calculate_diagnostics). */
+int ws_grid_set_field(ws_grid_t* grid, int32_t field, int32_t level, const void* host, int32_t height,
+                      int32_t width, int32_t dtype);
+int ws_grid_get_field(ws_grid_t* grid, int32_t field, int32_t level, void* host, int32_t height,
+                      int32_t width, int32_t dtype);
+/* Device address / row pitch (elements) / level stride (elements) of a field, for
+ * zero-copy interop (e.g. torch.from_dlpack-free views). */
+int ws_grid_device_field(ws_grid_t* grid, int32_t field, void** dptr, int64_t* pitch, int64_t* level_stride);
+/* Vorticity / divergence (weather_grid.cpp:82-121). Marks them due; the kernel runs when
+ * they are read (lazy), so a run() of N steps launches no diagnostics kernel. */
+int ws_grid_calculate_diagnostics(ws_grid_t* grid);
+/* InitialCondition::initialize(grid) for the registered names (initial_conditions.cpp:611-666):
+ * "uniform"(u,v,h,p,t,q) "random"(seed,amplitude) "zonal_flow"(u_max,h_mean,beta)
+ * "vortex"(x_center,y_center,radius,strength,h_mean) "jet_stream"(y_center,width,strength,h_mean)
+ * "breaking_wave"(amplitude,wavelength,h_mean) "front"(y_position,width,temp_difference,wind_shear)
+ * "mountain"(x_center,y_center,radius,height,u_base) "atmospheric_profile"(sparam = profile name).
+ * Missing trailing params take the reference defaults. level = -1 applies to every level. */
+int ws_grid_apply_initial_condition(ws_grid_t* grid, const char* name, const double* params, int32_t nparams,
+                                    const char* sparam, int32_t level);
+
+/* ---- WeatherSimulation ---------------------------------------------------------- */
+int ws_sim_create(const ws_config_t* cfg, ws_sim_t** out);
+int ws_sim_destroy(ws_sim_t* sim);
+/* which = 0: current grid, 1: next grid. The handle is a stable slot: after a step the
+ * simulation's current grid is the other slot (reference stale-handle semantics,
+ * SURVEY Appendix C.7). Grids are owned by the simulation. */
+int ws_sim_grid(ws_sim_t* sim, int32_t which, ws_grid_t** out);
+/* initialize() minus the IC: time = step = 0, metrics reset, current grid reset()
+ * (weather_simulation.cpp:46-66); the caller applies the IC to ws_sim_grid(sim, 0). */
+int ws_sim_initialize(ws_sim_t* sim);
+int ws_sim_step(ws_sim_t* sim);
+/* run(n) (weather_simulation.cpp:68-103): stops after the step at which t >= max_time.
+ * One call launches all steps on the device; *steps_taken may be NULL. */
+int ws_sim_run(ws_sim_t* sim, int32_t num_steps, int32_t* steps_taken);
+int ws_sim_run_until(ws_sim_t* sim, double max_time, int32_t* steps_taken);
+int ws_sim_get_time(const ws_sim_t* sim, double* t);
+int ws_sim_get_step(const ws_sim_t* sim, int32_t* step);
+int ws_sim_get_dt(const ws_sim_t* sim, double* dt);
+int ws_sim_set_dt(ws_sim_t* sim, double dt);
+int ws_sim_get_config(const ws_sim_t* sim, ws_config_t* cfg);
+int ws_sim_get_metrics(const ws_sim_t* sim, ws_metrics_t* m);
+int ws_sim_reset_metrics(ws_sim_t* sim);
+int ws_sim_synchronize(ws_sim_t* sim);
+/* Device milliseconds of the last ws_sim_run / ws_sim_run_until (hipEvents on the sim's
+ * stream) and the number of stage kernels it launched. */
+int ws_sim_last_run_stats(const ws_sim_t* sim, double* device_ms, int64_t* kernel_launches);
+
+/* ---- KernelAdapter plugin API (gpu_adaptability.hpp:242-329) --------------------- */
+/* One full forward-Euler step in -> out (the semantics of the reference's fused
+ * shallowWaterStepKernel_*), gravity / coriolis_f explicit, dx/dy from `in`. Writes u,v,h
+ * (+T,P for the PE model) of `out` and marks its diagnostics due. *ms = device time. */
+int ws_adapter_execute_shallow_water_step(ws_grid_t* in, ws_grid_t* out, double dt, double gravity,
+                                          double coriolis_f, double* ms);
+int ws_adapter_execute_barotropic_step(ws_grid_t* in, ws_grid_t* out, double dt, double gravity,
+                                       double coriolis_f, double* ms);
+int ws_adapter_execute_primitive_equations_step(ws_grid_t* in, ws_grid_t* out, double dt, double gravity,
+                                                double coriolis_f, double* ms);
+int ws_adapter_execute_gcm_step(ws_grid_t* in, ws_grid_t* out, double dt, double gravity, double coriolis_f,
+                                double* ms);
+int ws_adapter_calculate_diagnostics(ws_grid_t* grid, double* ms);
+
+/* ---- raw-pointer kernel ABI (shallow_water_kernels.cu:704-719, :830-840) ---------- */
+/* Caller-owned device buffers, row pitch in elements (>= width), one level, stream may
+ * be NULL (default stream). Asynchronous; returns WS_OK or WS_ERR_* on a launch error. */
+int ws_launch_shallow_water_kernel(const void* d_u, const void* d_v, const void* d_h, void* d_u_out,
+                                   void* d_v_out, void* d_h_out, int32_t width, int32_t height, int64_t pitch,
+                                   double dt, double gravity, double dx, double dy, double coriolis_f,
+                                   int32_t dtype, void* stream);
+int ws_launch_diagnostics_kernels(const void* d_u, const void* d_v, void* d_vorticity, void* d_divergence,
+                                  int32_t width, int32_t height, int64_t pitch, double dx, double dy,
+                                  int32_t dtype, void* stream);
+
+/* ---- slab decomposition over RCCL (new) ----------------------------------------- */
+#define WS_COMM_ID_BYTES 128
+int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]);
+/* One rank of a y-slab decomposition of the global grid described by cfg. Rank r owns
+ * rows [row0, row0 + rows) (balanced split, returned); halo rows are exchanged with
+ * ncclSend/ncclRecv between neighbouring ranks. Fields set / read through the slab's
+ * grids are the local rows only. Results are bitwise identical to one GPU. */
+int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
+                       ws_sim_t** out, int32_t* row0, int32_t* rows);
+
+/* Row range [row0, row0 + rows) of rank `rank` in the balanced split of `height` rows. */
+int ws_slab_partition(int32_t height, int32_t rank, int32_t nranks, int32_t* row0, int32_t* rows);
+/* Collectives on the slab communicator (max over ranks of one double; barrier). On a
+ * single-GPU simulation they are local no-ops. */
+int ws_sim_comm_allreduce_max(ws_sim_t* sim, double value, double* out);
+int ws_sim_comm_barrier(ws_sim_t* sim);
+
+/* ---- per-kernel timing (measurement) --------------------------------------------- */
+/* When enabled, every stage kernel of ws_sim_run / ws_sim_step is bracketed by hipEvents
+ * on the simulation's stream. kind = stage index within the step (0..3 for RK4). The
+ * statistics reset when timing is (re-)enabled. bytes_per_launch is the algorithmic
+ * HBM traffic of one launch (SURVEY §8(d) words x cells x element size). */
+int ws_sim_set_kernel_timing(ws_sim_t* sim, int32_t enable);
+int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, double* total_ms,
+                         double* bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WS_HIP_H */

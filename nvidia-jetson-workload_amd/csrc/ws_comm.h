@@ -1,0 +1,54 @@
+// y-slab halo exchange over RCCL (ncclSend / ncclRecv between neighbouring ranks).
+//
+// The reference has no distributed path; this is new. Rank r owns rows
+// [row0, row0 + H) of the global grid. Its `depth` top rows go to rank r-1 (which stores
+// them as rows [H', H'+depth) of its own buffers) and its `depth` bottom rows go to rank
+// r+1 (stored as rows [-depth, 0)). The global top / bottom edges keep the reference's
+// clamp-to-self stencil (Geom::top_clamp / bot_clamp), so no exchange happens there.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+
+#include "ws_internal.h"
+
+namespace ws {
+
+struct CommError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+// Balanced row partition: rank r owns [H*r/n, H*(r+1)/n).
+inline void slab_rows(int H, int rank, int nranks, int* row0, int* rows) {
+    const int r0 = (int)((int64_t)H * rank / nranks), r1 = (int)((int64_t)H * (rank + 1) / nranks);
+    *row0 = r0;
+    *rows = r1 - r0;
+}
+
+class SlabComm {
+public:
+    static void unique_id(uint8_t* id128);
+    SlabComm(int rank, int nranks, const uint8_t* id128);
+    ~SlabComm();
+    SlabComm(const SlabComm&) = delete;
+    SlabComm& operator=(const SlabComm&) = delete;
+
+    int rank() const { return rank_; }
+    int nranks() const { return nranks_; }
+
+    // Exchange `depth` halo rows of `nfields` level-stacked fields (row 0 of level 0 at
+    // fields[i]) with both neighbours, enqueued on `stream` as one grouped RCCL call.
+    void exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream);
+    // In-place max over ranks of one double (device scratch owned by the comm).
+    double allreduce_max(double v, hipStream_t stream);
+    void barrier(hipStream_t stream);
+
+private:
+    int rank_ = 0, nranks_ = 1;
+    void* comm_ = nullptr;  // ncclComm_t
+    double* scratch_ = nullptr;
+};
+
+}  // namespace ws

@@ -1,0 +1,973 @@
+// Host runtime of libws_hip.so: the C ABI declared in include/ws_hip.h.
+//
+// Owns device-resident grids (SoA, one allocation per field, rows padded to a 64-element
+// pitch, kHalo spare rows above/below each level for slab halos) and the time stepper that
+// replaces WeatherSimulation::step/run (reference src/weather-sim/cpp/src/
+// weather_simulation.cpp:68-158). Fields leave the device only through ws_grid_get_field.
+#include "ws_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ws_comm.h"
+#include "ws_ic.h"
+#include "ws_internal.h"
+#include "ws_timer.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct WsError : std::runtime_error {
+    int code;
+    WsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define WS_HIP_CHECK(expr)                                                                                \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess)                                                                             \
+            throw WsError(WS_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return WS_OK;
+    } catch (const WsError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const ws::CommError& e) {
+        g_last_error = e.what();
+        return WS_ERR_COMM;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of host memory";
+        return WS_ERR_DEVICE;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return WS_ERR_INVALID;
+    }
+}
+
+void require(bool cond, int code, const char* msg) {
+    if (!cond) throw WsError(code, msg);
+}
+
+int device_count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void set_device(int dev) {
+    const int n = device_count();
+    if (n <= 0) throw WsError(WS_ERR_DEVICE, "no HIP device available (MI355X build has no CPU path)");
+    if (dev < 0 || dev >= n) throw WsError(WS_ERR_DEVICE, "device_id out of range");
+    WS_HIP_CHECK(hipSetDevice(dev));
+}
+
+size_t elem_size(int dtype) { return dtype == WS_F64 ? 8 : 4; }
+
+bool is_pow2(double v) {
+    if (!(v > 0) || !std::isfinite(v)) return false;
+    int e;
+    return std::frexp(v, &e) == 0.5;
+}
+
+// value rounded to the simulation precision (the reference stores scalar_t)
+double to_prec(double v, int dtype) { return dtype == WS_F64 ? v : (double)(float)v; }
+
+}  // namespace
+
+struct ws_grid {
+    int32_t W = 0, H = 0, L = 1, dtype = WS_F32, device = 0;
+    int64_t pitch = 0, lstride = 0;
+    double dx = 1.0, dy = 1.0;  // already rounded to the grid precision
+    void* alloc[8] = {};
+    void* f[8] = {};            // row 0 of level 0
+    unsigned nfields = 8;
+    bool diag_pending = false;
+    bool owned = false;         // owned by a ws_sim
+    int32_t top_clamp = 1, bot_clamp = 1;
+    int32_t row0 = 0, gH = 0;   // slab: first global row, global height (ICs use global coordinates)
+    hipStream_t stream = nullptr;
+
+    ws::Geom geom() const {
+        ws::Geom g;
+        g.W = W; g.H = H; g.L = L; g.pitch = pitch; g.lstride = lstride;
+        g.top_clamp = top_clamp; g.bot_clamp = bot_clamp;
+        return g;
+    }
+    size_t bytes_per_field() const { return (size_t)L * lstride * elem_size(dtype); }
+};
+
+namespace {
+
+void grid_alloc(ws_grid* g, unsigned nfields) {
+    g->pitch = ((int64_t)g->W + 63) / 64 * 64;
+    g->lstride = ((int64_t)g->H + 2 * ws::kHalo) * g->pitch;
+    g->nfields = nfields;
+    const size_t es = elem_size(g->dtype);
+    for (unsigned i = 0; i < nfields; ++i) {
+        WS_HIP_CHECK(hipMalloc(&g->alloc[i], g->bytes_per_field()));
+        WS_HIP_CHECK(hipMemset(g->alloc[i], 0, g->bytes_per_field()));
+        g->f[i] = (char*)g->alloc[i] + (size_t)ws::kHalo * g->pitch * es;
+    }
+}
+
+void grid_free(ws_grid* g) {
+    for (auto& a : g->alloc)
+        if (a) { (void)hipFree(a); a = nullptr; }
+}
+
+template <typename T>
+ws::Spacing<T> make_spacing(double dx, double dy) {
+    ws::Spacing<T> s;
+    s.two_dx = T(2.0f) * (T)dx;
+    s.two_dy = T(2.0f) * (T)dy;
+    s.pow2x = is_pow2((double)s.two_dx);
+    s.pow2y = is_pow2((double)s.two_dy);
+    s.inv2dx = s.pow2x ? T(1) / s.two_dx : T(0);
+    s.inv2dy = s.pow2y ? T(1) / s.two_dy : T(0);
+    return s;
+}
+
+template <typename T>
+void grid_reset_t(ws_grid* g) {
+    const ws::Geom ge = g->geom();
+    // weather_grid.cpp:57-71 (float literals, widened for the fp64 build)
+    const T vals[8] = {T(0.0f), T(0.0f), T(10.0f), T(1013.25f), T(288.15f), T(0.0f), T(0.0f), T(0.0f)};
+    for (unsigned i = 0; i < g->nfields; ++i) WS_HIP_CHECK(ws::launch_fill<T>((T*)g->f[i], vals[i], ge, g->stream));
+    g->diag_pending = false;
+}
+
+void grid_reset(ws_grid* g) {
+    if (g->dtype == WS_F64) grid_reset_t<double>(g);
+    else grid_reset_t<float>(g);
+}
+
+template <typename T>
+void grid_diag_t(ws_grid* g) {
+    WS_HIP_CHECK(ws::launch_diagnostics<T>((const T*)g->f[WS_FIELD_U], (const T*)g->f[WS_FIELD_V],
+                                           (T*)g->f[WS_FIELD_VORTICITY], (T*)g->f[WS_FIELD_DIVERGENCE],
+                                           make_spacing<T>(g->dx, g->dy), g->geom(), g->stream));
+}
+
+// Run pending diagnostics now (lazy vorticity / divergence).
+void materialize_diag(ws_grid* g) {
+    if (!g->diag_pending) return;
+    if (g->dtype == WS_F64) grid_diag_t<double>(g);
+    else grid_diag_t<float>(g);
+    g->diag_pending = false;
+}
+
+ws_grid* new_grid(int32_t W, int32_t H, int32_t L, int32_t dtype, int32_t device, unsigned nfields, hipStream_t s) {
+    require(W > 0 && H > 0 && L > 0, WS_ERR_INVALID, "Grid dimensions must be positive");
+    require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "dtype must be WS_F32 or WS_F64");
+    set_device(device);
+    ws_grid* g = new ws_grid;
+    g->W = W; g->H = H; g->L = L; g->dtype = dtype; g->device = device; g->stream = s;
+    g->row0 = 0; g->gH = H;
+    try {
+        grid_alloc(g, nfields);
+        if (nfields == 8) grid_reset(g);
+    } catch (...) {
+        grid_free(g);
+        delete g;
+        throw;
+    }
+    return g;
+}
+
+template <typename Dst, typename Src>
+void convert(Dst* d, const Src* s, size_t n) {
+    for (size_t i = 0; i < n; ++i) d[i] = static_cast<Dst>(s[i]);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// simulation
+// ------------------------------------------------------------------------------------
+struct ws_sim {
+    ws_config_t cfg{};
+    int32_t dtype = WS_F32;
+    int32_t device = 0;
+    ws_grid* slot[2] = {nullptr, nullptr};
+    int cur = 0;
+    ws_grid* tmpA = nullptr;  // RK stage state ping-pong (u, v, h only)
+    ws_grid* tmpB = nullptr;
+    ws_grid* K2 = nullptr;    // RK4 stage-2 / stage-3 tendencies
+    ws_grid* K3 = nullptr;
+    double time = 0.0;        // rounded to the precision after every add
+    double dt = 0.01;
+    int32_t step = 0;
+    ws_metrics_t metrics{};
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0.0;
+    int64_t last_launches = 0;
+    ws::KernelTimer timer;
+    // slab decomposition
+    ws::SlabComm* comm = nullptr;
+    int32_t row0 = 0;
+};
+
+namespace {
+
+// Integrator actually executed (weather_simulation.cpp:122-142, :334-338, :457-471).
+int effective_method(const ws_config_t& c) {
+    switch (c.integration_method) {
+        case WS_RK2: return WS_RK2;
+        case WS_RK4: return c.model == WS_MODEL_SHALLOW_WATER ? WS_RK4 : WS_RK2;
+        default: return WS_EULER;
+    }
+}
+
+template <typename T>
+ws::StageArgs<T> stage_args(const ws_grid* in, const ws_grid* base, ws_grid* out, T c, const ws_sim* s) {
+    ws::StageArgs<T> a{};
+    a.in_u = (const T*)in->f[0]; a.in_v = (const T*)in->f[1]; a.in_h = (const T*)in->f[2];
+    a.base_u = (const T*)base->f[0]; a.base_v = (const T*)base->f[1]; a.base_h = (const T*)base->f[2];
+    a.out_u = (T*)out->f[0]; a.out_v = (T*)out->f[1]; a.out_h = (T*)out->f[2];
+    a.c = c;
+    a.gravity = (T)s->cfg.gravity;
+    a.coriolis_f = (T)s->cfg.coriolis_f;
+    a.sp = make_spacing<T>(in->dx, in->dy);
+    return a;
+}
+
+template <typename T>
+void launch(ws_sim* s, int mode, const ws::StageArgs<T>& a, const ws_grid* in, int kind, int words) {
+    if (s->comm) s->comm->exchange(in->f, 3, (int)sizeof(T), in->geom(), 1, s->stream);
+    const ws::Geom g = s->slot[0]->geom();
+    s->timer.begin(kind, (double)words * sizeof(T) * g.W * g.H * g.L, s->stream);
+    WS_HIP_CHECK(ws::launch_stage<T>(mode, a, g, s->stream));
+    s->timer.end(s->stream);
+    ++s->last_launches;
+}
+
+// One time step on the stream (no host synchronisation).
+template <typename T>
+void enqueue_step(ws_sim* s) {
+    ws_grid* c = s->slot[s->cur];
+    ws_grid* n = s->slot[1 - s->cur];
+    const T dt = (T)s->dt;
+    const T half = T(0.5f) * dt;  // `0.5f * dt_` (weather_simulation.cpp:249)
+    const int method = effective_method(s->cfg);
+    if (method == WS_EULER) {
+        launch<T>(s, ws::kAxpy, stage_args<T>(c, c, n, dt, s), c, 0, 6);
+    } else if (method == WS_RK2) {
+        launch<T>(s, ws::kAxpy, stage_args<T>(c, c, s->tmpA, half, s), c, 0, 6);
+        launch<T>(s, ws::kAxpy, stage_args<T>(s->tmpA, c, n, dt, s), s->tmpA, 1, 9);
+    } else {
+        launch<T>(s, ws::kAxpy, stage_args<T>(c, c, s->tmpA, half, s), c, 0, 6);
+        auto a2 = stage_args<T>(s->tmpA, c, s->tmpB, half, s);
+        a2.k2_u = (T*)s->K2->f[0]; a2.k2_v = (T*)s->K2->f[1]; a2.k2_h = (T*)s->K2->f[2];
+        launch<T>(s, ws::kAxpyStore, a2, s->tmpA, 1, 12);
+        auto a3 = stage_args<T>(s->tmpB, c, s->tmpA, dt, s);
+        a3.k2_u = (T*)s->K3->f[0]; a3.k2_v = (T*)s->K3->f[1]; a3.k2_h = (T*)s->K3->f[2];
+        launch<T>(s, ws::kAxpyStore, a3, s->tmpB, 2, 12);
+        auto a4 = stage_args<T>(s->tmpA, c, n, dt / T(6.0f), s);  // `dt_ / 6.0f`
+        a4.k2_u = (T*)s->K2->f[0]; a4.k2_v = (T*)s->K2->f[1]; a4.k2_h = (T*)s->K2->f[2];
+        a4.k3_u = (const T*)s->K3->f[0]; a4.k3_v = (const T*)s->K3->f[1]; a4.k3_h = (const T*)s->K3->f[2];
+        launch<T>(s, ws::kRk4Final, a4, s->tmpA, 3, 15);
+    }
+    if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
+        // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
+        const ws::Geom g = c->geom();
+        WS_HIP_CHECK(ws::launch_affine<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], dt, T(288.15f), g, s->stream));
+        WS_HIP_CHECK(ws::launch_affine<T>((T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], dt, T(1013.25f), g, s->stream));
+        s->last_launches += 2;
+    }
+    s->cur = 1 - s->cur;
+    s->slot[s->cur]->diag_pending = true;  // step() ends with calculateDiagnostics (:149)
+}
+
+template <typename T>
+double advance_time(double t, double dt) {
+    T tt = (T)t;
+    tt += (T)dt;
+    return (double)tt;
+}
+
+// Decide on the host how many of n steps run(n) takes (weather_simulation.cpp:77-90).
+int plan_steps(const ws_sim* s, int n) {
+    if (n <= 0) return 0;
+    const bool f64 = s->dtype == WS_F64;
+    const double max_time = to_prec(s->cfg.max_time, s->dtype);
+    double t = s->time;
+    int k = 0;
+    while (k < n) {
+        t = f64 ? advance_time<double>(t, s->dt) : advance_time<float>(t, s->dt);
+        ++k;
+        if (t >= max_time) break;
+    }
+    return k;
+}
+
+void run_steps(ws_sim* s, int k) {
+    set_device(s->device);
+    s->last_launches = 0;
+    WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
+    for (int i = 0; i < k; ++i) {
+        if (s->dtype == WS_F64) enqueue_step<double>(s);
+        else enqueue_step<float>(s);
+        s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
+        s->step++;
+    }
+    WS_HIP_CHECK(hipEventRecord(s->ev1, s->stream));
+    WS_HIP_CHECK(hipEventSynchronize(s->ev1));
+    s->timer.collect();
+    float ms = 0.f;
+    WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last_ms = ms;
+    s->metrics.compute_time_ms += ms;
+    s->metrics.total_time_ms += ms;
+    s->metrics.num_steps += k;
+}
+
+void sim_free(ws_sim* s) {
+    for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
+        if (g) { grid_free(g); delete g; }
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s->comm;
+    delete s;
+}
+
+ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm, int32_t row0) {
+    require(cfg != nullptr, WS_ERR_INVALID, "null config");
+    require(cfg->grid_width > 0 && cfg->grid_height > 0 && cfg->num_levels > 0, WS_ERR_INVALID,
+            "Grid dimensions must be positive");
+    require(cfg->dx > 0 && cfg->dy > 0, WS_ERR_INVALID, "Grid spacing must be positive");
+    set_device(cfg->device_id);
+    ws_sim* s = new ws_sim;
+    s->cfg = *cfg;
+    s->dtype = cfg->double_precision ? WS_F64 : WS_F32;
+    s->device = cfg->device_id;
+    s->dt = to_prec(cfg->dt, s->dtype);
+    s->comm = comm;
+    s->row0 = row0;
+    try {
+        WS_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        WS_HIP_CHECK(hipEventCreate(&s->ev0));
+        WS_HIP_CHECK(hipEventCreate(&s->ev1));
+        const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
+        for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
+        const int method = effective_method(*cfg);
+        if (method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
+        if (method == WS_RK4) {
+            s->tmpB = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
+            s->K2 = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
+            s->K3 = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
+        }
+        for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3}) {
+            if (!g) continue;
+            g->owned = true;
+            g->dx = to_prec(cfg->dx, s->dtype);
+            g->dy = to_prec(cfg->dy, s->dtype);
+            if (comm) {
+                g->top_clamp = comm->rank() == 0;
+                g->bot_clamp = comm->rank() == comm->nranks() - 1;
+                g->row0 = row0;
+                g->gH = cfg->grid_height;
+            }
+        }
+        WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    } catch (...) {
+        s->comm = nullptr;  // caller keeps ownership on failure
+        sim_free(s);
+        throw;
+    }
+    return s;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------
+extern "C" {
+
+const char* ws_last_error(void) { return g_last_error.c_str(); }
+
+int ws_abi_version(void) { return WS_ABI_VERSION; }
+
+int ws_is_available(int32_t* available) {
+    return guarded([&] {
+        require(available != nullptr, WS_ERR_INVALID, "null pointer");
+        *available = device_count() > 0;
+    });
+}
+
+int ws_device_count(int32_t* count) {
+    return guarded([&] {
+        require(count != nullptr, WS_ERR_INVALID, "null pointer");
+        *count = device_count();
+    });
+}
+
+int ws_device_info(int32_t device, ws_device_info_t* out) {
+    return guarded([&] {
+        require(out != nullptr, WS_ERR_INVALID, "null pointer");
+        set_device(device);
+        hipDeviceProp_t p;
+        WS_HIP_CHECK(hipGetDeviceProperties(&p, device));
+        std::memset(out, 0, sizeof(*out));
+        std::snprintf(out->device_name, sizeof(out->device_name), "%s", p.name);
+        std::snprintf(out->arch, sizeof(out->arch), "%s", p.gcnArchName);
+        out->compute_capability_major = p.major;
+        out->compute_capability_minor = p.minor;
+        out->multiprocessors = p.multiProcessorCount;
+        out->cuda_cores = p.multiProcessorCount * 64;
+        out->global_memory = (int64_t)p.totalGlobalMem;
+        out->shared_memory_per_block = (int32_t)p.sharedMemPerBlock;
+        out->max_threads_per_block = p.maxThreadsPerBlock;
+        out->max_threads_per_multiprocessor = p.maxThreadsPerMultiProcessor;
+        out->clock_rate_khz = p.clockRate;
+        out->memory_clock_rate_khz = p.memoryClockRate;
+        out->memory_bus_width = p.memoryBusWidth;
+        out->wavefront_size = p.warpSize;
+    });
+}
+
+void ws_config_default(ws_config_t* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    // SimulationConfig defaults (weather_sim.hpp:155-191)
+    c->model = WS_MODEL_SHALLOW_WATER;
+    c->grid_type = 1;  // Staggered
+    c->integration_method = WS_RK4;
+    c->boundary_condition = 0;  // Periodic (accepted, not read: clamp-to-self)
+    c->grid_width = 256;
+    c->grid_height = 256;
+    c->num_levels = 1;
+    c->dx = 1.0; c->dy = 1.0; c->dt = 0.01;
+    c->gravity = 9.81; c->coriolis_f = 0.0;
+    c->compute_backend = WS_BACKEND_CUDA;
+    c->double_precision = 0;
+    c->device_id = 0;
+    c->num_threads = 0;
+    c->max_time = 10.0;
+    c->max_steps = 1000;
+    c->output_interval = 10;
+    c->random_seed = 0;
+}
+
+// ---- grid ----
+int ws_grid_create(int32_t width, int32_t height, int32_t num_levels, int32_t dtype, int32_t device,
+                   ws_grid_t** out) {
+    return guarded([&] {
+        require(out != nullptr, WS_ERR_INVALID, "null pointer");
+        ws_grid* g = new_grid(width, height, num_levels, dtype, device, 8, nullptr);
+        WS_HIP_CHECK(hipStreamSynchronize(nullptr));
+        *out = g;
+    });
+}
+
+int ws_grid_destroy(ws_grid_t* g) {
+    return guarded([&] {
+        if (!g) return;
+        require(!g->owned, WS_ERR_INVALID, "grid is owned by a simulation");
+        set_device(g->device);
+        grid_free(g);
+        delete g;
+    });
+}
+
+int ws_grid_reset(ws_grid_t* g) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        set_device(g->device);
+        grid_reset(g);
+        WS_HIP_CHECK(hipStreamSynchronize(g->stream));
+    });
+}
+
+int ws_grid_get_dims(const ws_grid_t* g, int32_t* w, int32_t* h, int32_t* l, int32_t* dt) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        if (w) *w = g->W;
+        if (h) *h = g->H;
+        if (l) *l = g->L;
+        if (dt) *dt = g->dtype;
+    });
+}
+
+int ws_grid_set_spacing(ws_grid_t* g, double dx, double dy) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        require(dx > 0.0 && dy > 0.0, WS_ERR_INVALID, "Grid spacing must be positive");
+        g->dx = to_prec(dx, g->dtype);
+        g->dy = to_prec(dy, g->dtype);
+    });
+}
+
+int ws_grid_get_spacing(const ws_grid_t* g, double* dx, double* dy) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        if (dx) *dx = g->dx;
+        if (dy) *dy = g->dy;
+    });
+}
+
+static void check_field_args(const ws_grid* g, int32_t field, int32_t level, int32_t height, int32_t width,
+                             int32_t dtype, bool writing) {
+    require(g != nullptr, WS_ERR_INVALID, "null grid");
+    require(field >= 0 && field < (int)g->nfields, WS_ERR_INVALID, "bad field id");
+    require(!writing || field < WS_FIELD_VORTICITY, WS_ERR_INVALID, "diagnostic fields are read-only");
+    require(level >= -1 && level < g->L, WS_ERR_INVALID, "level out of range");
+    require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "dtype must be WS_F32 or WS_F64");
+    require(height == g->H && width == g->W, WS_ERR_SHAPE, "Array dimensions must match field dimensions");
+}
+
+static void copy_field(ws_grid* g, int32_t field, int32_t level, void* host, int32_t dtype, bool to_device) {
+    const size_t es = elem_size(g->dtype), n = (size_t)g->W * g->H;
+    const int l0 = level < 0 ? 0 : level, l1 = level < 0 ? g->L : level + 1;
+    std::vector<char> tmp;
+    for (int l = l0; l < l1; ++l) {
+        char* hp = (char*)host + (size_t)(l - l0) * n * elem_size(dtype);
+        void* src_or_dst = hp;
+        if (dtype != g->dtype) {
+            tmp.resize(n * es);
+            src_or_dst = tmp.data();
+            if (to_device) {
+                if (g->dtype == WS_F32) convert((float*)tmp.data(), (const double*)hp, n);
+                else convert((double*)tmp.data(), (const float*)hp, n);
+            }
+        }
+        char* dev = (char*)g->f[field] + (size_t)l * g->lstride * es;
+        if (to_device)
+            WS_HIP_CHECK(hipMemcpy2DAsync(dev, g->pitch * es, src_or_dst, g->W * es, g->W * es, g->H,
+                                          hipMemcpyHostToDevice, g->stream));
+        else
+            WS_HIP_CHECK(hipMemcpy2DAsync(src_or_dst, g->W * es, dev, g->pitch * es, g->W * es, g->H,
+                                          hipMemcpyDeviceToHost, g->stream));
+        WS_HIP_CHECK(hipStreamSynchronize(g->stream));
+        if (!to_device && dtype != g->dtype) {
+            if (g->dtype == WS_F32) convert((double*)hp, (const float*)tmp.data(), n);
+            else convert((float*)hp, (const double*)tmp.data(), n);
+        }
+    }
+}
+
+int ws_grid_set_field(ws_grid_t* g, int32_t field, int32_t level, const void* host, int32_t height, int32_t width,
+                      int32_t dtype) {
+    return guarded([&] {
+        check_field_args(g, field, level, height, width, dtype, true);
+        require(host != nullptr, WS_ERR_INVALID, "null host pointer");
+        set_device(g->device);
+        // keep vorticity what calculateDiagnostics made of the OLD u, v (reference setters
+        // do not recompute diagnostics)
+        if (field == WS_FIELD_U || field == WS_FIELD_V) materialize_diag(g);
+        copy_field(g, field, level, const_cast<void*>(host), dtype, true);
+    });
+}
+
+int ws_grid_get_field(ws_grid_t* g, int32_t field, int32_t level, void* host, int32_t height, int32_t width,
+                      int32_t dtype) {
+    return guarded([&] {
+        check_field_args(g, field, level, height, width, dtype, false);
+        require(host != nullptr, WS_ERR_INVALID, "null host pointer");
+        set_device(g->device);
+        if (field >= WS_FIELD_VORTICITY) materialize_diag(g);
+        copy_field(g, field, level, host, dtype, false);
+    });
+}
+
+int ws_grid_device_field(ws_grid_t* g, int32_t field, void** dptr, int64_t* pitch, int64_t* level_stride) {
+    return guarded([&] {
+        require(g != nullptr && field >= 0 && field < (int)g->nfields, WS_ERR_INVALID, "bad grid/field");
+        set_device(g->device);
+        if (field >= WS_FIELD_VORTICITY) {
+            materialize_diag(g);
+            WS_HIP_CHECK(hipStreamSynchronize(g->stream));
+        }
+        if (dptr) *dptr = g->f[field];
+        if (pitch) *pitch = g->pitch;
+        if (level_stride) *level_stride = g->lstride;
+    });
+}
+
+int ws_grid_calculate_diagnostics(ws_grid_t* g) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        g->diag_pending = true;
+    });
+}
+
+int ws_grid_apply_initial_condition(ws_grid_t* g, const char* name, const double* params, int32_t nparams,
+                                    const char* sparam, int32_t level) {
+    return guarded([&] {
+        require(g != nullptr && name != nullptr, WS_ERR_INVALID, "null argument");
+        require(level >= -1 && level < g->L, WS_ERR_INVALID, "level out of range");
+        set_device(g->device);
+        const std::string nm(name), sp(sparam ? sparam : "");
+        auto apply = [&](auto tag) {
+            using T = decltype(tag);
+            ws::IcFields<T> f(g->W, g->gH, g->row0, g->H);
+            require(ws::compute_initial_condition<T>(nm, params, nparams, sp, f), WS_ERR_INVALID,
+                    "unknown initial condition");
+            materialize_diag(g);
+            const std::pair<unsigned, std::vector<T>*> m[6] = {{ws::kU, &f.u}, {ws::kV, &f.v}, {ws::kH, &f.h},
+                                                               {ws::kP, &f.p}, {ws::kT, &f.t}, {ws::kQ, &f.q}};
+            const int l0 = level < 0 ? 0 : level, l1 = level < 0 ? g->L : level + 1;
+            for (int i = 0; i < 6; ++i)
+                if (f.wrote & m[i].first)
+                    for (int l = l0; l < l1; ++l) copy_field(g, i, l, m[i].second->data(), g->dtype, true);
+        };
+        if (g->dtype == WS_F64) apply(double{});
+        else apply(float{});
+        g->diag_pending = true;  // every IC ends with grid.calculateDiagnostics()
+    });
+}
+
+// ---- simulation ----
+int ws_sim_create(const ws_config_t* cfg, ws_sim_t** out) {
+    return guarded([&] {
+        require(out != nullptr, WS_ERR_INVALID, "null pointer");
+        *out = sim_build(cfg, cfg ? cfg->grid_height : 0, nullptr, 0);
+    });
+}
+
+int ws_sim_destroy(ws_sim_t* s) {
+    return guarded([&] {
+        if (!s) return;
+        set_device(s->device);
+        (void)hipStreamSynchronize(s->stream);
+        sim_free(s);
+    });
+}
+
+int ws_sim_grid(ws_sim_t* s, int32_t which, ws_grid_t** out) {
+    return guarded([&] {
+        require(s != nullptr && out != nullptr && (which == 0 || which == 1), WS_ERR_INVALID, "bad argument");
+        *out = s->slot[which == 0 ? s->cur : 1 - s->cur];
+    });
+}
+
+int ws_sim_initialize(ws_sim_t* s) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        set_device(s->device);
+        s->time = 0.0;
+        s->step = 0;
+        std::memset(&s->metrics, 0, sizeof(s->metrics));
+        grid_reset(s->slot[s->cur]);
+        WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int ws_sim_step(ws_sim_t* s) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        run_steps(s, 1);
+    });
+}
+
+int ws_sim_run(ws_sim_t* s, int32_t n, int32_t* taken) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        const int k = plan_steps(s, n);
+        if (k > 0) run_steps(s, k);
+        if (taken) *taken = k;
+    });
+}
+
+int ws_sim_run_until(ws_sim_t* s, double max_time, int32_t* taken) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        int k = 0;
+        // weather_simulation.cpp:105-115, evaluated in scalar_t
+        if (s->dtype == WS_F64) {
+            const double mt = max_time, t = s->time;
+            if (!(mt <= t)) k = plan_steps(s, (int)((mt - t) / s->dt) + 1);
+        } else {
+            const float mt = (float)max_time, t = (float)s->time;
+            if (!(mt <= t)) k = plan_steps(s, (int)((mt - t) / (float)s->dt) + 1);
+        }
+        if (k > 0) run_steps(s, k);
+        if (taken) *taken = k;
+    });
+}
+
+int ws_sim_get_time(const ws_sim_t* s, double* t) {
+    return guarded([&] {
+        require(s && t, WS_ERR_INVALID, "null pointer");
+        *t = s->time;
+    });
+}
+
+int ws_sim_get_step(const ws_sim_t* s, int32_t* st) {
+    return guarded([&] {
+        require(s && st, WS_ERR_INVALID, "null pointer");
+        *st = s->step;
+    });
+}
+
+int ws_sim_get_dt(const ws_sim_t* s, double* dt) {
+    return guarded([&] {
+        require(s && dt, WS_ERR_INVALID, "null pointer");
+        *dt = s->dt;
+    });
+}
+
+int ws_sim_set_dt(ws_sim_t* s, double dt) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        s->dt = to_prec(dt, s->dtype);
+    });
+}
+
+int ws_sim_get_config(const ws_sim_t* s, ws_config_t* cfg) {
+    return guarded([&] {
+        require(s && cfg, WS_ERR_INVALID, "null pointer");
+        *cfg = s->cfg;
+    });
+}
+
+int ws_sim_get_metrics(const ws_sim_t* s, ws_metrics_t* m) {
+    return guarded([&] {
+        require(s && m, WS_ERR_INVALID, "null pointer");
+        *m = s->metrics;
+    });
+}
+
+int ws_sim_reset_metrics(ws_sim_t* s) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        std::memset(&s->metrics, 0, sizeof(s->metrics));
+    });
+}
+
+int ws_sim_synchronize(ws_sim_t* s) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        set_device(s->device);
+        WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int ws_sim_last_run_stats(const ws_sim_t* s, double* ms, int64_t* launches) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        if (ms) *ms = s->last_ms;
+        if (launches) *launches = s->last_launches;
+    });
+}
+
+// ---- KernelAdapter ----
+static int adapter_step(ws_grid* in, ws_grid* out, double dt, double g, double f, double* ms, bool pe) {
+    return guarded([&] {
+        require(in && out && in != out, WS_ERR_INVALID, "in and out must be distinct grids");
+        require(in->W == out->W && in->H == out->H && in->L == out->L && in->dtype == out->dtype &&
+                    in->device == out->device && out->nfields == 8,
+                WS_ERR_SHAPE, "grids must have identical dimensions and precision");
+        set_device(in->device);
+        hipEvent_t e0, e1;
+        WS_HIP_CHECK(hipEventCreate(&e0));
+        WS_HIP_CHECK(hipEventCreate(&e1));
+        auto body = [&](auto tag) {
+            using T = decltype(tag);
+            ws::StageArgs<T> a{};
+            a.in_u = (const T*)in->f[0]; a.in_v = (const T*)in->f[1]; a.in_h = (const T*)in->f[2];
+            a.base_u = a.in_u; a.base_v = a.in_v; a.base_h = a.in_h;
+            a.out_u = (T*)out->f[0]; a.out_v = (T*)out->f[1]; a.out_h = (T*)out->f[2];
+            a.c = (T)dt; a.gravity = (T)g; a.coriolis_f = (T)f;
+            a.sp = make_spacing<T>(in->dx, in->dy);
+            WS_HIP_CHECK(ws::launch_stage<T>(ws::kAxpy, a, in->geom(), in->stream));
+            if (pe) {
+                WS_HIP_CHECK(ws::launch_affine<T>((T*)out->f[WS_FIELD_T], (const T*)in->f[WS_FIELD_T], (T)dt,
+                                                  T(288.15f), in->geom(), in->stream));
+                WS_HIP_CHECK(ws::launch_affine<T>((T*)out->f[WS_FIELD_P], (const T*)in->f[WS_FIELD_P], (T)dt,
+                                                  T(1013.25f), in->geom(), in->stream));
+            }
+        };
+        WS_HIP_CHECK(hipEventRecord(e0, in->stream));
+        if (in->dtype == WS_F64) body(double{});
+        else body(float{});
+        WS_HIP_CHECK(hipEventRecord(e1, in->stream));
+        WS_HIP_CHECK(hipEventSynchronize(e1));
+        float t = 0.f;
+        WS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        out->diag_pending = true;
+        if (ms) *ms = t;
+    });
+}
+
+int ws_adapter_execute_shallow_water_step(ws_grid_t* in, ws_grid_t* out, double dt, double g, double f, double* ms) {
+    return adapter_step(in, out, dt, g, f, ms, false);
+}
+int ws_adapter_execute_barotropic_step(ws_grid_t* in, ws_grid_t* out, double dt, double g, double f, double* ms) {
+    return adapter_step(in, out, dt, g, f, ms, false);
+}
+int ws_adapter_execute_primitive_equations_step(ws_grid_t* in, ws_grid_t* out, double dt, double g, double f,
+                                                double* ms) {
+    return adapter_step(in, out, dt, g, f, ms, true);
+}
+int ws_adapter_execute_gcm_step(ws_grid_t* in, ws_grid_t* out, double dt, double g, double f, double* ms) {
+    return adapter_step(in, out, dt, g, f, ms, false);
+}
+
+int ws_adapter_calculate_diagnostics(ws_grid_t* g, double* ms) {
+    return guarded([&] {
+        require(g != nullptr, WS_ERR_INVALID, "null grid");
+        set_device(g->device);
+        hipEvent_t e0, e1;
+        WS_HIP_CHECK(hipEventCreate(&e0));
+        WS_HIP_CHECK(hipEventCreate(&e1));
+        WS_HIP_CHECK(hipEventRecord(e0, g->stream));
+        g->diag_pending = true;
+        materialize_diag(g);
+        WS_HIP_CHECK(hipEventRecord(e1, g->stream));
+        WS_HIP_CHECK(hipEventSynchronize(e1));
+        float t = 0.f;
+        WS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (ms) *ms = t;
+    });
+}
+
+// ---- raw kernel ABI ----
+int ws_launch_shallow_water_kernel(const void* d_u, const void* d_v, const void* d_h, void* d_u_out, void* d_v_out,
+                                   void* d_h_out, int32_t width, int32_t height, int64_t pitch, double dt,
+                                   double gravity, double dx, double dy, double coriolis_f, int32_t dtype,
+                                   void* stream) {
+    return guarded([&] {
+        require(d_u && d_v && d_h && d_u_out && d_v_out && d_h_out, WS_ERR_INVALID, "null device pointer");
+        require(width > 0 && height > 0 && pitch >= width, WS_ERR_INVALID, "bad dimensions");
+        require(dx > 0 && dy > 0, WS_ERR_INVALID, "Grid spacing must be positive");
+        ws::Geom g{};
+        g.W = width; g.H = height; g.L = 1; g.pitch = pitch; g.lstride = pitch * height;
+        g.top_clamp = 1; g.bot_clamp = 1;
+        auto body = [&](auto tag) {
+            using T = decltype(tag);
+            ws::StageArgs<T> a{};
+            a.in_u = (const T*)d_u; a.in_v = (const T*)d_v; a.in_h = (const T*)d_h;
+            a.base_u = a.in_u; a.base_v = a.in_v; a.base_h = a.in_h;
+            a.out_u = (T*)d_u_out; a.out_v = (T*)d_v_out; a.out_h = (T*)d_h_out;
+            a.c = (T)dt; a.gravity = (T)gravity; a.coriolis_f = (T)coriolis_f;
+            a.sp = make_spacing<T>(to_prec(dx, dtype), to_prec(dy, dtype));
+            WS_HIP_CHECK(ws::launch_stage<T>(ws::kAxpy, a, g, (hipStream_t)stream));
+        };
+        require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "bad dtype");
+        if (dtype == WS_F64) body(double{});
+        else body(float{});
+    });
+}
+
+int ws_launch_diagnostics_kernels(const void* d_u, const void* d_v, void* d_vort, void* d_div, int32_t width,
+                                  int32_t height, int64_t pitch, double dx, double dy, int32_t dtype, void* stream) {
+    return guarded([&] {
+        require(d_u && d_v && d_vort && d_div, WS_ERR_INVALID, "null device pointer");
+        require(width > 0 && height > 0 && pitch >= width, WS_ERR_INVALID, "bad dimensions");
+        require(dx > 0 && dy > 0, WS_ERR_INVALID, "Grid spacing must be positive");
+        require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "bad dtype");
+        ws::Geom g{};
+        g.W = width; g.H = height; g.L = 1; g.pitch = pitch; g.lstride = pitch * height;
+        g.top_clamp = 1; g.bot_clamp = 1;
+        if (dtype == WS_F64)
+            WS_HIP_CHECK(ws::launch_diagnostics<double>((const double*)d_u, (const double*)d_v, (double*)d_vort,
+                                                        (double*)d_div, make_spacing<double>(dx, dy), g,
+                                                        (hipStream_t)stream));
+        else
+            WS_HIP_CHECK(ws::launch_diagnostics<float>((const float*)d_u, (const float*)d_v, (float*)d_vort,
+                                                       (float*)d_div, make_spacing<float>((float)dx, (float)dy), g,
+                                                       (hipStream_t)stream));
+    });
+}
+
+// ---- slab decomposition ----
+int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]) {
+    return guarded([&] {
+        require(id != nullptr, WS_ERR_INVALID, "null pointer");
+        ws::SlabComm::unique_id(id);
+    });
+}
+
+int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
+                       ws_sim_t** out, int32_t* row0, int32_t* rows) {
+    return guarded([&] {
+        require(cfg && id && out, WS_ERR_INVALID, "null pointer");
+        require(nranks >= 1 && rank >= 0 && rank < nranks, WS_ERR_INVALID, "bad rank / nranks");
+        require(cfg->grid_height >= nranks, WS_ERR_INVALID, "fewer rows than ranks");
+        int r0 = 0, nrows = 0;
+        ws::slab_rows(cfg->grid_height, rank, nranks, &r0, &nrows);
+        const int r1 = r0 + nrows;
+        set_device(cfg->device_id);
+        ws::SlabComm* comm = new ws::SlabComm(rank, nranks, id);
+        ws_sim* s = nullptr;
+        try {
+            s = sim_build(cfg, r1 - r0, comm, r0);
+        } catch (...) {
+            delete comm;
+            throw;
+        }
+        *out = s;
+        if (row0) *row0 = r0;
+        if (rows) *rows = r1 - r0;
+    });
+}
+
+int ws_slab_partition(int32_t height, int32_t rank, int32_t nranks, int32_t* row0, int32_t* rows) {
+    return guarded([&] {
+        require(row0 && rows, WS_ERR_INVALID, "null pointer");
+        require(nranks >= 1 && rank >= 0 && rank < nranks && height >= nranks, WS_ERR_INVALID, "bad partition");
+        int r0 = 0, n = 0;
+        ws::slab_rows(height, rank, nranks, &r0, &n);
+        *row0 = r0;
+        *rows = n;
+    });
+}
+
+int ws_sim_comm_allreduce_max(ws_sim_t* s, double value, double* out) {
+    return guarded([&] {
+        require(s && out, WS_ERR_INVALID, "null pointer");
+        set_device(s->device);
+        *out = s->comm ? s->comm->allreduce_max(value, s->stream) : value;
+    });
+}
+
+int ws_sim_set_kernel_timing(ws_sim_t* s, int32_t enable) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        s->timer.enable(enable != 0);
+        s->timer.reset();
+    });
+}
+
+int ws_sim_kernel_timing(const ws_sim_t* s, int32_t kind, int64_t* launches, double* total_ms,
+                         double* bytes_per_launch) {
+    return guarded([&] {
+        require(s != nullptr && kind >= 0 && kind < ws::KernelTimer::kKinds, WS_ERR_INVALID, "bad argument");
+        const auto& st = s->timer.stat(kind);
+        if (launches) *launches = st.launches;
+        if (total_ms) *total_ms = st.total_ms;
+        if (bytes_per_launch) *bytes_per_launch = st.bytes_per_launch;
+    });
+}
+
+int ws_sim_comm_barrier(ws_sim_t* s) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        set_device(s->device);
+        if (s->comm) s->comm->barrier(s->stream);
+        WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    });
+}
+
+}  // extern "C"

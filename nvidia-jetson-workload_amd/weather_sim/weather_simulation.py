@@ -1,0 +1,995 @@
+"""Weather Simulation Python API -- MI355X-native drop-in for the reference module.
+
+Mirrors /root/reference/src/weather-sim/python/weather_simulation.py (the high-level
+wrapper and helpers) and the names that module imports from the pybind module
+`pyweather_sim` (src/weather-sim/cpp/src/python_bindings.cpp:116-372): same class names,
+method names, argument meanings, defaults and error types. Underneath, every grid lives in
+MI355X HBM and every step runs as hand-written HIP kernels through libws_hip.so (the C ABI
+in include/ws_hip.h). There is no CPU compute path and no mock fallback.
+
+Deliberate deviations from the reference (documented in DESIGN.md):
+  * ComputeBackend is accepted and recorded, but every backend runs the HIP path (the
+    reference's CUDA branch was an empty placeholder, weather_simulation.cpp:492-500).
+  * SimulationConfig.double_precision is honoured (fp64 grids); fp32 is the default and
+    matches the reference bit-for-bit.
+  * num_levels > 1 stores [L, H, W] fields of independent 2-D levels (the reference
+    ignores num_levels, weather_grid.cpp:36-48); getters then return (L, H, W) arrays.
+  * PerformanceMetrics times are device milliseconds, not integer-truncated host ms.
+  * Vorticity / divergence are computed lazily (when read), with identical values.
+"""
+import ctypes
+import os
+import random
+import time
+from enum import IntEnum
+from typing import Dict, List, Optional, Union
+
+import numpy as np
+
+from . import _native
+from ._native import FIELD, WS_F32, WS_F64, check, lib
+
+VERBOSE = os.environ.get("WS_QUIET", "0") in ("", "0")
+
+
+def _say(msg):
+    if VERBOSE:
+        print(msg)
+
+
+# ---------------------------------------------------------------------------------
+# Enumerations (weather_sim.hpp:30-76, python_bindings.cpp:120-171)
+# ---------------------------------------------------------------------------------
+class SimulationModel(IntEnum):
+    ShallowWater = 0
+    Barotropic = 1
+    PrimitiveEquations = 2
+    General = 3
+
+
+class IntegrationMethod(IntEnum):
+    ExplicitEuler = 0
+    RungeKutta2 = 1
+    RungeKutta4 = 2
+    AdamsBashforth = 3
+    SemiImplicit = 4
+
+
+class GridType(IntEnum):
+    Cartesian = 0
+    Staggered = 1
+    Icosahedral = 2
+    SphericalHarmonic = 3
+
+
+class BoundaryCondition(IntEnum):
+    Periodic = 0
+    Reflective = 1
+    Outflow = 2
+    Custom = 3
+
+
+class ComputeBackend(IntEnum):
+    CUDA = 0  # kept as the GPU value for API compatibility: the HIP device
+    CPU = 1
+    Hybrid = 2
+    AdaptiveHybrid = 3
+
+
+class DeviceType(IntEnum):
+    Unknown = 0
+    CPU = 1
+    JetsonOrinNX = 2
+    T4 = 3
+    HighEndGPU = 4
+    OtherGPU = 5
+
+
+class OutputFormat(IntEnum):
+    CSV = 0
+    NetCDF = 1
+    VTK = 2
+    PNG = 3
+    Custom = 4
+
+
+# ---------------------------------------------------------------------------------
+# Structures
+# ---------------------------------------------------------------------------------
+class SimulationConfig:
+    """SimulationConfig (weather_sim.hpp:155-191) with the C++ defaults."""
+
+    def __init__(self):
+        self.model = SimulationModel.ShallowWater
+        self.grid_type = GridType.Staggered
+        self.integration_method = IntegrationMethod.RungeKutta4
+        self.boundary_condition = BoundaryCondition.Periodic
+        self.grid_width = 256
+        self.grid_height = 256
+        self.num_levels = 1
+        self.dx = 1.0
+        self.dy = 1.0
+        self.dt = 0.01
+        self.gravity = 9.81
+        self.coriolis_f = 0.0
+        self.beta = 0.0
+        self.viscosity = 0.0
+        self.diffusivity = 0.0
+        self.compute_backend = ComputeBackend.CUDA
+        self.double_precision = False
+        self.device_id = 0
+        self.num_threads = 0
+        self.max_time = 10.0
+        self.max_steps = 1000
+        self.output_interval = 10
+        self.output_path = "./output"
+        self.random_seed = random.SystemRandom().getrandbits(32)  # std::random_device{}()
+
+    def _to_c(self):
+        c = _native.ws_config_t()
+        for name, _ in _native.ws_config_t._fields_:
+            setattr(c, name, type(getattr(c, name))(getattr(self, name)))
+        return c
+
+    @classmethod
+    def _from_c(cls, c, output_path="./output"):
+        self = cls()
+        for name, _ in _native.ws_config_t._fields_:
+            setattr(self, name, getattr(c, name))
+        self.model = SimulationModel(self.model)
+        self.integration_method = IntegrationMethod(self.integration_method)
+        self.grid_type = GridType(self.grid_type)
+        self.boundary_condition = BoundaryCondition(self.boundary_condition)
+        self.compute_backend = ComputeBackend(self.compute_backend)
+        self.double_precision = bool(self.double_precision)
+        self.output_path = output_path
+        return self
+
+    def __repr__(self):
+        return f"SimulationConfig({self.grid_width}x{self.grid_height}x{self.num_levels}, model={self.model!r}, " \
+               f"method={self.integration_method!r}, dt={self.dt}, fp64={self.double_precision})"
+
+
+class PerformanceMetrics:
+    """PerformanceMetrics (weather_sim.hpp:196-223)."""
+
+    def __init__(self):
+        self.total_time_ms = 0.0
+        self.compute_time_ms = 0.0
+        self.memory_transfer_time_ms = 0.0
+        self.io_time_ms = 0.0
+        self.num_steps = 0
+
+    def reset(self):
+        self.__init__()
+
+    def print(self):
+        t = self.total_time_ms or float("nan")
+        print("Performance Metrics:")
+        print(f"  Total time: {self.total_time_ms} ms")
+        print(f"  Compute time: {self.compute_time_ms} ms ({self.compute_time_ms / t * 100.0}%)")
+        print(f"  Memory transfer time: {self.memory_transfer_time_ms} ms ({self.memory_transfer_time_ms / t * 100.0}%)")
+        print(f"  I/O time: {self.io_time_ms} ms ({self.io_time_ms / t * 100.0}%)")
+        print(f"  Steps: {self.num_steps}")
+        print(f"  Time per step: {self.total_time_ms / self.num_steps if self.num_steps else float('nan')} ms")
+
+
+class OutputConfig:
+    """OutputConfig (output_manager.hpp:35-97); the file writers are out of scope."""
+
+    def __init__(self):
+        self.output_dir = "./output"
+        self.prefix = "weather_sim"
+        self.format = OutputFormat.CSV
+        self.output_interval = 10
+        self.compress = False
+        self.include_diagnostics = True
+        self.fields = ["velocity", "height", "vorticity"]
+
+
+class DeviceCapabilities:
+    """DeviceCapabilities (gpu_adaptability.hpp:35-88) for the HIP device."""
+
+    def __init__(self, info=None):
+        self.device_type = DeviceType.Unknown
+        self.device_name = "Unknown"
+        self.arch = ""
+        self.compute_capability_major = 0
+        self.compute_capability_minor = 0
+        self.cuda_cores = 0
+        self.multiprocessors = 0
+        self.global_memory = 0
+        self.shared_memory_per_block = 0
+        self.max_threads_per_block = 0
+        self.max_threads_per_multiprocessor = 0
+        self.clock_rate_khz = 0
+        self.memory_clock_rate_khz = 0
+        self.memory_bus_width = 0
+        self.compute_power_ratio = 0.0
+        if info is not None:
+            for name, _ in _native.ws_device_info_t._fields_:
+                v = getattr(info, name)
+                setattr(self, name, v.decode() if isinstance(v, bytes) else v)
+            self.device_type = DeviceType.HighEndGPU
+            self.compute_power_ratio = 1.0
+
+    def get_summary(self):
+        return (f"Device: {self.device_name} ({self.arch}), CUs: {self.multiprocessors}, "
+                f"Memory: {self.global_memory / 2**30:.1f} GiB, wavefront 64")
+
+
+# ---------------------------------------------------------------------------------
+# WeatherGrid (weather_sim.hpp:254-412; python_bindings.cpp:240-284)
+# ---------------------------------------------------------------------------------
+class WeatherGrid:
+    """A device-resident grid. `WeatherGrid(width, height, num_levels=1)` or
+    `WeatherGrid(config)`; extension keywords: double_precision, device_id."""
+
+    def __init__(self, width, height=None, num_levels=1, *, double_precision=False, device_id=0, _handle=None,
+                 _owner=None):
+        self._owner = _owner  # keeps the owning simulation alive
+        if _handle is not None:
+            self._h = ctypes.c_void_p(_handle)
+            self._owned = False
+        else:
+            dx = dy = None
+            if isinstance(width, SimulationConfig):
+                cfg = width
+                width, height, num_levels = cfg.grid_width, cfg.grid_height, cfg.num_levels
+                double_precision, device_id = cfg.double_precision, cfg.device_id
+                dx, dy = cfg.dx, cfg.dy
+            if height is None:
+                raise TypeError("WeatherGrid(width, height, num_levels=1) or WeatherGrid(config)")
+            h = ctypes.c_void_p()
+            check(lib.ws_grid_create(int(width), int(height), int(num_levels), WS_F64 if double_precision else WS_F32,
+                                     int(device_id), ctypes.byref(h)))
+            self._h = h
+            self._owned = True
+            if dx is not None:
+                check(lib.ws_grid_set_spacing(self._h, float(dx), float(dy)))
+        w, hh, l, dt = (ctypes.c_int32() for _ in range(4))
+        check(lib.ws_grid_get_dims(self._h, ctypes.byref(w), ctypes.byref(hh), ctypes.byref(l), ctypes.byref(dt)))
+        self._W, self._H, self._L = w.value, hh.value, l.value
+        self._dtype = np.float64 if dt.value == WS_F64 else np.float32
+        self._ws_dtype = dt.value
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and self._h:
+            lib.ws_grid_destroy(self._h)
+            self._h = None
+
+    # -- dimensions / spacing
+    def reset(self):
+        check(lib.ws_grid_reset(self._h))
+
+    def get_width(self):
+        return self._W
+
+    def get_height(self):
+        return self._H
+
+    def get_num_levels(self):
+        return self._L
+
+    def get_dx(self):
+        dx, dy = ctypes.c_double(), ctypes.c_double()
+        check(lib.ws_grid_get_spacing(self._h, ctypes.byref(dx), ctypes.byref(dy)))
+        return dx.value
+
+    def get_dy(self):
+        dx, dy = ctypes.c_double(), ctypes.c_double()
+        check(lib.ws_grid_get_spacing(self._h, ctypes.byref(dx), ctypes.byref(dy)))
+        return dy.value
+
+    def set_spacing(self, dx, dy):
+        check(lib.ws_grid_set_spacing(self._h, float(dx), float(dy)))
+
+    def calculate_diagnostics(self):
+        check(lib.ws_grid_calculate_diagnostics(self._h))
+
+    @property
+    def dtype(self):
+        return self._dtype
+
+    # -- field copies (python_bindings.cpp:22-114)
+    def _get(self, name, level=None):
+        lvl = -1 if level is None else int(level)
+        shape = (self._H, self._W) if (self._L == 1 or lvl >= 0) else (self._L, self._H, self._W)
+        if self._L == 1 and lvl == -1:
+            lvl = 0
+        out = np.empty(shape, self._dtype)
+        check(lib.ws_grid_get_field(self._h, FIELD[name], lvl, out.ctypes.data, self._H, self._W, self._ws_dtype))
+        return out
+
+    def _set(self, name, arr, level=None):
+        a = np.asarray(arr)
+        if level is not None:
+            lvl = int(level)
+            want_ndim = 2
+        elif self._L > 1 and a.ndim == 3:
+            lvl, want_ndim = -1, 3
+        else:
+            lvl, want_ndim = (-1 if self._L > 1 else 0), 2
+        if a.ndim != want_ndim:
+            raise RuntimeError(f"Number of dimensions must be {want_ndim}")
+        if a.shape[-2:] != (self._H, self._W) or (want_ndim == 3 and a.shape[0] != self._L):
+            raise RuntimeError("Array dimensions must match field dimensions")
+        if want_ndim == 2 and lvl == -1:  # one (H, W) array for every level
+            a = np.broadcast_to(a, (self._L, self._H, self._W))
+        a = np.ascontiguousarray(a, dtype=self._dtype)
+        check(lib.ws_grid_set_field(self._h, FIELD[name], lvl, a.ctypes.data, self._H, self._W, self._ws_dtype))
+
+    def get_velocity_field(self, level=None):
+        return self._get("u", level), self._get("v", level)
+
+    def get_height_field(self, level=None):
+        return self._get("h", level)
+
+    def get_pressure_field(self, level=None):
+        return self._get("p", level)
+
+    def get_temperature_field(self, level=None):
+        return self._get("t", level)
+
+    def get_humidity_field(self, level=None):
+        return self._get("q", level)
+
+    def get_vorticity_field(self, level=None):
+        return self._get("vorticity", level)
+
+    def get_divergence_field(self, level=None):
+        """Extension: the reference computes divergence but binds no getter."""
+        return self._get("divergence", level)
+
+    def set_velocity_field(self, u, v, level=None):
+        # reference checks both arrays before writing (python_bindings.cpp:92-104)
+        for a in (u, v):
+            a = np.asarray(a)
+            if a.ndim not in (2, 3):
+                raise RuntimeError("Number of dimensions must be 2")
+            if a.shape[-2:] != (self._H, self._W):
+                raise RuntimeError("Array dimensions must match field dimensions")
+        self._set("u", u, level)
+        self._set("v", v, level)
+
+    def set_height_field(self, h, level=None):
+        self._set("h", h, level)
+
+    def set_pressure_field(self, p, level=None):
+        self._set("p", p, level)
+
+    def set_temperature_field(self, t, level=None):
+        self._set("t", t, level)
+
+    def set_humidity_field(self, q, level=None):
+        self._set("q", q, level)
+
+    def device_field(self, name):
+        """Extension: (device pointer, row pitch, level stride) of a field, for zero-copy interop."""
+        p, pitch, ls = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib.ws_grid_device_field(self._h, FIELD[name], ctypes.byref(p), ctypes.byref(pitch), ctypes.byref(ls)))
+        return p.value, pitch.value, ls.value
+
+
+# ---------------------------------------------------------------------------------
+# Initial conditions (initial_conditions.hpp / initial_conditions.cpp:48-666)
+# ---------------------------------------------------------------------------------
+class InitialCondition:
+    _ws_name = None
+
+    def __init__(self, *params, sparam=""):
+        self._params = [float(p) for p in params]
+        self._sparam = sparam
+
+    def initialize(self, grid: WeatherGrid, level: Optional[int] = None):
+        arr = (ctypes.c_double * max(1, len(self._params)))(*self._params)
+        check(lib.ws_grid_apply_initial_condition(grid._h, self._ws_name.encode(), arr, len(self._params),
+                                                  self._sparam.encode(), -1 if level is None else int(level)))
+
+    def get_name(self):
+        return self._ws_name
+
+
+class UniformInitialCondition(InitialCondition):
+    _ws_name = "uniform"
+
+    def __init__(self, u=0.0, v=0.0, h=10.0, p=1000.0, t=300.0, q=0.0):
+        super().__init__(u, v, h, p, t, q)
+
+
+class RandomInitialCondition(InitialCondition):
+    _ws_name = "random"
+
+    def __init__(self, seed=0, amplitude=1.0):
+        super().__init__(int(seed) & 0xFFFFFFFF, amplitude)
+
+
+class ZonalFlowInitialCondition(InitialCondition):
+    _ws_name = "zonal_flow"
+
+    def __init__(self, u_max=10.0, h_mean=10.0, beta=0.1):
+        super().__init__(u_max, h_mean, beta)
+
+
+class VortexInitialCondition(InitialCondition):
+    _ws_name = "vortex"
+
+    def __init__(self, x_center=0.5, y_center=0.5, radius=0.1, strength=10.0, h_mean=10.0):
+        super().__init__(x_center, y_center, radius, strength, h_mean)
+
+
+class JetStreamInitialCondition(InitialCondition):
+    _ws_name = "jet_stream"
+
+    def __init__(self, y_center=0.5, width=0.1, strength=10.0, h_mean=10.0):
+        super().__init__(y_center, width, strength, h_mean)
+
+
+class BreakingWaveInitialCondition(InitialCondition):
+    _ws_name = "breaking_wave"
+
+    def __init__(self, amplitude=1.0, wavelength=0.2, h_mean=10.0):
+        super().__init__(amplitude, wavelength, h_mean)
+
+
+class FrontInitialCondition(InitialCondition):
+    _ws_name = "front"
+
+    def __init__(self, y_position=0.5, width=0.05, temp_difference=10.0, wind_shear=5.0):
+        super().__init__(y_position, width, temp_difference, wind_shear)
+
+
+class MountainInitialCondition(InitialCondition):
+    _ws_name = "mountain"
+
+    def __init__(self, x_center=0.3, y_center=0.5, radius=0.1, height=1.0, u_base=5.0):
+        super().__init__(x_center, y_center, radius, height, u_base)
+
+
+class AtmosphericProfileInitialCondition(InitialCondition):
+    _ws_name = "atmospheric_profile"
+
+    def __init__(self, profile_name="standard"):
+        super().__init__(sparam=profile_name)
+
+
+class InitialConditionFactory:
+    """Singleton registry (initial_conditions.cpp:16-45)."""
+    _instance = None
+
+    def __init__(self):
+        self._creators = {}
+
+    @classmethod
+    def get_instance(cls):
+        if cls._instance is None:
+            cls._instance = cls()
+        return cls._instance
+
+    def register_initial_condition(self, name, creator):
+        self._creators[name] = creator
+
+    def create_initial_condition(self, name):
+        c = self._creators.get(name)
+        return c() if c else None
+
+    def get_available_initial_conditions(self):
+        return sorted(self._creators)  # std::map iteration order
+
+
+def register_all_initial_conditions():
+    """initial_conditions.cpp:611-666"""
+    f = InitialConditionFactory.get_instance()
+    f.register_initial_condition("uniform", UniformInitialCondition)
+    f.register_initial_condition("random", RandomInitialCondition)
+    f.register_initial_condition("zonal_flow", ZonalFlowInitialCondition)
+    f.register_initial_condition("vortex", VortexInitialCondition)
+    f.register_initial_condition("jet_stream", JetStreamInitialCondition)
+    f.register_initial_condition("breaking_wave", BreakingWaveInitialCondition)
+    f.register_initial_condition("front", FrontInitialCondition)
+    f.register_initial_condition("mountain", MountainInitialCondition)
+    f.register_initial_condition("standard_atmosphere", lambda: AtmosphericProfileInitialCondition("standard"))
+    f.register_initial_condition("tropical_atmosphere", lambda: AtmosphericProfileInitialCondition("tropical"))
+    f.register_initial_condition("polar_atmosphere", lambda: AtmosphericProfileInitialCondition("polar"))
+
+
+# ---------------------------------------------------------------------------------
+# Output manager interface (weather_sim.hpp:549-570)
+# ---------------------------------------------------------------------------------
+class OutputManager:
+    def initialize(self, simulation):
+        pass
+
+    def write_output(self, simulation):
+        pass
+
+    def finalize(self, simulation):
+        pass
+
+
+# ---------------------------------------------------------------------------------
+# WeatherSimulation (weather_sim.hpp:417-544; weather_simulation.cpp)
+# ---------------------------------------------------------------------------------
+_BACKEND_NAMES = {0: "HIP GPU (MI355X)", 1: "HIP GPU (MI355X; CPU requested)", 2: "HIP GPU (MI355X; hybrid requested)",
+                  3: "HIP GPU (MI355X; adaptive hybrid requested)"}
+
+
+class WeatherSimulation:
+    def __init__(self, config: SimulationConfig, _slab=None):
+        self._config_py = config
+        c = config._to_c()
+        h = ctypes.c_void_p()
+        self.row0, self.rows = 0, config.grid_height
+        if _slab is None:
+            check(lib.ws_sim_create(ctypes.byref(c), ctypes.byref(h)))
+        else:
+            rank, nranks, uid = _slab
+            r0, nr = ctypes.c_int32(), ctypes.c_int32()
+            idbuf = (ctypes.c_uint8 * _native.COMM_ID_BYTES).from_buffer_copy(uid)
+            check(lib.ws_sim_create_slab(ctypes.byref(c), int(rank), int(nranks), idbuf, ctypes.byref(h),
+                                         ctypes.byref(r0), ctypes.byref(nr)))
+            self.row0, self.rows = r0.value, nr.value
+        self._h = h
+        self._ic = None
+        self._om = None
+        _say(f"Using compute backend: {_BACKEND_NAMES.get(int(config.compute_backend), 'HIP GPU (MI355X)')}")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.ws_sim_destroy(self._h)
+            self._h = None
+
+    def set_initial_condition(self, initial_condition):
+        self._ic = initial_condition
+
+    def set_output_manager(self, output_manager):
+        self._om = output_manager
+
+    def initialize(self):
+        check(lib.ws_sim_initialize(self._h))
+        if self._ic is not None:
+            self._ic.initialize(self.get_current_grid())
+        if self._om is not None:
+            self._om.initialize(self)
+
+    def step(self):
+        check(lib.ws_sim_step(self._h))
+
+    def _run_native(self, n):
+        taken = ctypes.c_int32()
+        check(lib.ws_sim_run(self._h, int(n), ctypes.byref(taken)))
+        return taken.value
+
+    def run(self, num_steps):
+        """weather_simulation.cpp:68-103 (stops after the step at which t >= max_time)."""
+        if num_steps <= 0:
+            return 0
+        t0 = time.perf_counter()
+        if self._om is None:
+            taken = self._run_native(num_steps)
+        else:  # output every output_interval steps needs the state between steps
+            taken = 0
+            interval = self._config_py.output_interval
+            for _ in range(num_steps):
+                t_before = self.get_current_step()
+                self._run_native(1)
+                taken += 1
+                if interval > 0 and self.get_current_step() % interval == 0:
+                    self._om.write_output(self)
+                if self.get_current_step() == t_before or self.get_current_time() >= self._max_time():
+                    break
+        ms = (time.perf_counter() - t0) * 1000.0
+        _say(f"Completed {num_steps} steps in {ms:.0f} ms ({ms / num_steps} ms/step)")
+        return taken
+
+    def _max_time(self):
+        return float(np.float64(self._config_py.max_time) if self._config_py.double_precision
+                     else np.float32(self._config_py.max_time))
+
+    def run_until(self, max_time):
+        """weather_simulation.cpp:105-115: run(int((T - t) / dt) + 1)."""
+        if self._om is not None:
+            dtype = np.float64 if self._config_py.double_precision else np.float32
+            T, t, dt = dtype(max_time), dtype(self.get_current_time()), dtype(self.get_dt())
+            if T <= t:
+                return 0
+            return self.run(int((T - t) / dt) + 1)
+        taken = ctypes.c_int32()
+        check(lib.ws_sim_run_until(self._h, float(max_time), ctypes.byref(taken)))
+        return taken.value
+
+    def get_current_time(self):
+        t = ctypes.c_double()
+        check(lib.ws_sim_get_time(self._h, ctypes.byref(t)))
+        return t.value
+
+    def get_current_step(self):
+        s = ctypes.c_int32()
+        check(lib.ws_sim_get_step(self._h, ctypes.byref(s)))
+        return s.value
+
+    def get_dt(self):
+        d = ctypes.c_double()
+        check(lib.ws_sim_get_dt(self._h, ctypes.byref(d)))
+        return d.value
+
+    def set_dt(self, dt):
+        check(lib.ws_sim_set_dt(self._h, float(dt)))
+
+    def get_config(self):
+        c = _native.ws_config_t()
+        check(lib.ws_sim_get_config(self._h, ctypes.byref(c)))
+        return SimulationConfig._from_c(c, self._config_py.output_path)
+
+    def get_current_grid(self):
+        g = ctypes.c_void_p()
+        check(lib.ws_sim_grid(self._h, 0, ctypes.byref(g)))
+        return WeatherGrid(None, _handle=g.value, _owner=self)
+
+    def get_performance_metrics(self):
+        m = _native.ws_metrics_t()
+        check(lib.ws_sim_get_metrics(self._h, ctypes.byref(m)))
+        out = PerformanceMetrics()
+        for name, _ in _native.ws_metrics_t._fields_:
+            setattr(out, name, getattr(m, name))
+        return out
+
+    def reset_performance_metrics(self):
+        check(lib.ws_sim_reset_metrics(self._h))
+
+    # -- extensions
+    def synchronize(self):
+        check(lib.ws_sim_synchronize(self._h))
+
+    def last_run_stats(self):
+        """(device ms, kernel launches) of the last run()/run_until()/step()."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        check(lib.ws_sim_last_run_stats(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def set_kernel_timing(self, enable=True):
+        check(lib.ws_sim_set_kernel_timing(self._h, 1 if enable else 0))
+
+    def kernel_timing(self):
+        """{stage kind: (launches, total device ms, algorithmic bytes per launch)}"""
+        out = {}
+        for k in range(8):
+            n, ms, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+            check(lib.ws_sim_kernel_timing(self._h, k, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(b)))
+            if n.value:
+                out[k] = (n.value, ms.value, b.value)
+        return out
+
+    def comm_allreduce_max(self, value):
+        out = ctypes.c_double()
+        check(lib.ws_sim_comm_allreduce_max(self._h, float(value), ctypes.byref(out)))
+        return out.value
+
+    def comm_barrier(self):
+        check(lib.ws_sim_comm_barrier(self._h))
+
+
+# ---------------------------------------------------------------------------------
+# KernelAdapter plugin API (gpu_adaptability.hpp:242-379)
+# ---------------------------------------------------------------------------------
+class KernelAdapter:
+    def initialize(self, device_id=0):
+        raise NotImplementedError
+
+    def is_compatible(self):
+        raise NotImplementedError
+
+    def get_name(self):
+        raise NotImplementedError
+
+    def get_priority(self):
+        raise NotImplementedError
+
+
+class HIPKernelAdapter(KernelAdapter):
+    """The MI355X adapter: one forward-Euler step in -> out per call (the semantics of the
+    reference's fused shallowWaterStepKernel_*). Returns device milliseconds; -1.0 when
+    not initialized (HybridExecutionManager::executeHybridStep convention)."""
+
+    def __init__(self, gravity=9.81, coriolis_f=0.0):
+        self.gravity, self.coriolis_f = gravity, coriolis_f
+        self._ready = False
+
+    def initialize(self, device_id=0):
+        self._ready = _native.is_available() and 0 <= device_id < _native.device_count()
+        return self._ready
+
+    def is_compatible(self):
+        return _native.is_available()
+
+    def get_name(self):
+        return "HIPAdapter"
+
+    def get_priority(self):
+        return 100
+
+    def _exec(self, fn, in_grid, out_grid, dt):
+        if not self._ready:
+            return -1.0
+        ms = ctypes.c_double()
+        check(fn(in_grid._h, out_grid._h, float(dt), float(self.gravity), float(self.coriolis_f), ctypes.byref(ms)))
+        return ms.value
+
+    def execute_shallow_water_step(self, in_grid, out_grid, dt):
+        return self._exec(lib.ws_adapter_execute_shallow_water_step, in_grid, out_grid, dt)
+
+    def execute_barotropic_step(self, in_grid, out_grid, dt):
+        return self._exec(lib.ws_adapter_execute_barotropic_step, in_grid, out_grid, dt)
+
+    def execute_primitive_equations_step(self, in_grid, out_grid, dt):
+        return self._exec(lib.ws_adapter_execute_primitive_equations_step, in_grid, out_grid, dt)
+
+    def execute_gcm_step(self, in_grid, out_grid, dt):
+        return self._exec(lib.ws_adapter_execute_gcm_step, in_grid, out_grid, dt)
+
+    def calculate_diagnostics(self, grid):
+        if not self._ready:
+            return -1.0
+        ms = ctypes.c_double()
+        check(lib.ws_adapter_calculate_diagnostics(grid._h, ctypes.byref(ms)))
+        return ms.value
+
+
+class KernelAdapterFactory:
+    """gpu_adaptability.cpp:544-592"""
+    _instance = None
+
+    def __init__(self):
+        self._adapters = []
+
+    @classmethod
+    def get_instance(cls):
+        if cls._instance is None:
+            cls._instance = cls()
+            cls._instance.register_adapter(HIPKernelAdapter())
+        return cls._instance
+
+    def register_adapter(self, adapter):
+        self._adapters.append(adapter)
+
+    def get_best_adapter(self, device_id=0):
+        best = None
+        for a in self._adapters:
+            if a.is_compatible() and (best is None or a.get_priority() > best.get_priority()):
+                best = a
+        if best is not None:
+            best.initialize(device_id)
+        return best
+
+    def get_adapter(self, name, device_id=0):
+        for a in self._adapters:
+            if a.get_name() == name:
+                a.initialize(device_id)
+                return a
+        return None
+
+    def get_available_adapters(self):
+        return [a.get_name() for a in self._adapters]
+
+
+class AdaptiveKernelManager:
+    """AdaptiveKernelManager (gpu_adaptability.hpp:128-237) reduced to what the Python API
+    uses: device detection and capabilities. There is one device kind, so workload ratios
+    are 1.0 (all on the GPU) and the optimal backend is the GPU."""
+    _instance = None
+
+    def __init__(self):
+        self._caps = DeviceCapabilities()
+        self._init = False
+
+    @classmethod
+    def get_instance(cls):
+        if cls._instance is None:
+            cls._instance = cls()
+        return cls._instance
+
+    def initialize(self, device_id=0):
+        if _native.is_available():
+            info = _native.ws_device_info_t()
+            check(lib.ws_device_info(int(device_id), ctypes.byref(info)))
+            self._caps = DeviceCapabilities(info)
+        else:
+            self._caps = DeviceCapabilities()
+            self._caps.device_type = DeviceType.CPU
+        self._init = True
+        return True
+
+    def is_cuda_available(self):
+        return _native.is_available()
+
+    def get_device_capabilities(self):
+        if not self._init:
+            self.initialize()
+        return self._caps
+
+    def get_gpu_workload_ratio(self, *args, **kwargs):
+        return 1.0 if self.is_cuda_available() else 0.0
+
+    def determine_optimal_backend(self, *args, **kwargs):
+        return ComputeBackend.CUDA
+
+
+# ---------------------------------------------------------------------------------
+# High-level wrapper (weather_simulation.py:194-371)
+# ---------------------------------------------------------------------------------
+class WeatherSimulationWrapper:
+    """High-level wrapper for the Weather Simulation."""
+
+    def __init__(self, width: int = 256, height: int = 256, model: Union[str, int] = "shallow_water", dt: float = 0.01,
+                 integration_method: Union[str, int] = "rk4", backend: Union[str, int] = "adaptive",
+                 device_id: int = 0, threads: int = 0, output_interval: int = 10, output_path: str = "./output",
+                 double_precision: bool = False, num_levels: int = 1):
+        self.config = SimulationConfig()
+        self.config.grid_width = width
+        self.config.grid_height = height
+        self.config.dt = dt
+        self.config.output_interval = output_interval
+        self.config.output_path = output_path
+        self.config.device_id = device_id
+        self.config.num_threads = threads
+        self.config.double_precision = double_precision
+        self.config.num_levels = num_levels
+        if isinstance(model, str):
+            model_map = {"shallow_water": SimulationModel.ShallowWater, "barotropic": SimulationModel.Barotropic,
+                         "primitive": SimulationModel.PrimitiveEquations, "general": SimulationModel.General}
+            self.config.model = model_map.get(model.lower(), SimulationModel.ShallowWater)
+        else:
+            self.config.model = model
+        if isinstance(integration_method, str):
+            method_map = {"euler": IntegrationMethod.ExplicitEuler, "rk2": IntegrationMethod.RungeKutta2,
+                          "rk4": IntegrationMethod.RungeKutta4, "adams_bashforth": IntegrationMethod.AdamsBashforth,
+                          "semi_implicit": IntegrationMethod.SemiImplicit}
+            self.config.integration_method = method_map.get(integration_method.lower(), IntegrationMethod.RungeKutta4)
+        else:
+            self.config.integration_method = integration_method
+        if isinstance(backend, str):
+            backend_map = {"cuda": ComputeBackend.CUDA, "cpu": ComputeBackend.CPU, "hybrid": ComputeBackend.Hybrid,
+                           "adaptive": ComputeBackend.AdaptiveHybrid, "hip": ComputeBackend.CUDA}
+            self.config.compute_backend = backend_map.get(backend.lower(), ComputeBackend.AdaptiveHybrid)
+        else:
+            self.config.compute_backend = backend
+        self.simulation = WeatherSimulation(self.config)
+        self.initialized = False
+        self.output_data = []
+
+    def set_initial_condition(self, condition_name: str, **kwargs):
+        initial_condition = create_initial_condition(condition_name, **kwargs)
+        if initial_condition:
+            self.simulation.set_initial_condition(initial_condition)
+
+    def initialize(self):
+        self.simulation.initialize()
+        self.initialized = True
+
+    def step(self):
+        if not self.initialized:
+            self.initialize()
+        self.simulation.step()
+        if self.config.output_interval > 0 and self.simulation.get_current_step() % self.config.output_interval == 0:
+            self._store_output()
+
+    def run(self, steps: int):
+        if not self.initialized:
+            self.initialize()
+        start_time = time.time()
+        self.simulation.run(steps)
+        end_time = time.time()
+        elapsed = (end_time - start_time) * 1000
+        _say(f"Completed {steps} steps in {elapsed:.2f} ms ({elapsed / steps:.2f} ms/step)")
+
+    def run_until(self, max_time: float):
+        if not self.initialized:
+            self.initialize()
+        start_time = time.time()
+        self.simulation.run_until(max_time)
+        end_time = time.time()
+        steps = self.simulation.get_current_step()
+        elapsed = (end_time - start_time) * 1000
+        _say(f"Reached time {max_time} in {elapsed:.2f} ms ({elapsed / steps:.2f} ms/step)")
+
+    def get_grid(self):
+        return self.simulation.get_current_grid()
+
+    def get_metrics(self):
+        return self.simulation.get_performance_metrics()
+
+    def get_output_data(self):
+        return self.output_data
+
+    def _store_output(self):
+        grid = self.simulation.get_current_grid()
+        snapshot = {
+            'time': self.simulation.get_current_time(),
+            'step': self.simulation.get_current_step(),
+            'u': grid.get_velocity_field()[0].copy(),
+            'v': grid.get_velocity_field()[1].copy(),
+            'height': grid.get_height_field().copy(),
+            'vorticity': grid.get_vorticity_field().copy(),
+        }
+        self.output_data.append(snapshot)
+
+
+# ---------------------------------------------------------------------------------
+# Helper functions (weather_simulation.py:376-520)
+# ---------------------------------------------------------------------------------
+def create_initial_condition(name: str, **kwargs) -> Optional[object]:
+    try:
+        if name == "uniform":
+            return UniformInitialCondition(kwargs.get("u", 0.0), kwargs.get("v", 0.0), kwargs.get("h", 10.0),
+                                           kwargs.get("p", 1000.0), kwargs.get("t", 300.0), kwargs.get("q", 0.0))
+        elif name == "random":
+            return RandomInitialCondition(kwargs.get("seed", 0), kwargs.get("amplitude", 1.0))
+        elif name == "zonal_flow":
+            return ZonalFlowInitialCondition(kwargs.get("u_max", 10.0), kwargs.get("h_mean", 10.0),
+                                             kwargs.get("beta", 0.1))
+        elif name == "vortex":
+            return VortexInitialCondition(kwargs.get("x_center", 0.5), kwargs.get("y_center", 0.5),
+                                          kwargs.get("radius", 0.1), kwargs.get("strength", 10.0),
+                                          kwargs.get("h_mean", 10.0))
+        elif name == "jet_stream":
+            return JetStreamInitialCondition(kwargs.get("y_center", 0.5), kwargs.get("width", 0.1),
+                                             kwargs.get("strength", 10.0), kwargs.get("h_mean", 10.0))
+        elif name == "breaking_wave":
+            return BreakingWaveInitialCondition(kwargs.get("amplitude", 1.0), kwargs.get("wavelength", 0.2),
+                                                kwargs.get("h_mean", 10.0))
+        elif name == "front":
+            return FrontInitialCondition(kwargs.get("y_position", 0.5), kwargs.get("width", 0.05),
+                                         kwargs.get("temp_difference", 10.0), kwargs.get("wind_shear", 5.0))
+        elif name == "mountain":
+            return MountainInitialCondition(kwargs.get("x_center", 0.3), kwargs.get("y_center", 0.5),
+                                            kwargs.get("radius", 0.1), kwargs.get("height", 1.0),
+                                            kwargs.get("u_base", 5.0))
+        elif name == "atmospheric_profile":
+            return AtmosphericProfileInitialCondition(kwargs.get("profile_name", "standard"))
+        else:
+            return InitialConditionFactory.get_instance().create_initial_condition(name)
+    except Exception as e:  # reference prints and returns None
+        print(f"Error creating initial condition '{name}': {e}")
+        return None
+
+
+def get_available_initial_conditions() -> List[str]:
+    try:
+        return InitialConditionFactory.get_instance().get_available_initial_conditions()
+    except Exception:
+        return ["uniform", "random", "zonal_flow", "vortex", "jet_stream", "breaking_wave", "front", "mountain",
+                "atmospheric_profile"]
+
+
+def is_cuda_available() -> bool:
+    """True when the HIP device (MI355X) is usable."""
+    try:
+        return AdaptiveKernelManager.get_instance().is_cuda_available()
+    except Exception:
+        return False
+
+
+def get_device_info() -> Dict:
+    try:
+        manager = AdaptiveKernelManager.get_instance()
+        manager.initialize()
+        capabilities = manager.get_device_capabilities()
+        device_type_map = {DeviceType.Unknown: "Unknown", DeviceType.CPU: "CPU",
+                           DeviceType.JetsonOrinNX: "Jetson Orin NX", DeviceType.T4: "NVIDIA T4",
+                           DeviceType.HighEndGPU: "High-End GPU", DeviceType.OtherGPU: "Other GPU"}
+        return {
+            "device_type": device_type_map.get(capabilities.device_type, "Unknown"),
+            "device_name": capabilities.device_name,
+            "compute_capability": f"{capabilities.compute_capability_major}.{capabilities.compute_capability_minor}",
+            "cuda_cores": capabilities.cuda_cores,
+            "multiprocessors": capabilities.multiprocessors,
+            "global_memory_mb": capabilities.global_memory / (1024 * 1024),
+            "compute_power_ratio": capabilities.compute_power_ratio,
+            "cuda_available": manager.is_cuda_available(),
+            "arch": capabilities.arch,
+        }
+    except Exception as e:
+        return {"device_type": "Unknown", "device_name": "Unknown", "error": str(e), "cuda_available": False}
+
+
+register_all_initial_conditions()

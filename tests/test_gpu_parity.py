@@ -1,0 +1,265 @@
+"""HIP path vs the reference, through the C ABI (weather_sim -> libws_hip.so). GPU only.
+
+Small cases compare bit-for-bit (max-ulp 0, fp32 AND fp64) with the reference's own
+outputs in tests/golden/ref_small_*.npz: every (model, method, IC, spacing/physics) case
+after 1, 10 and 50 steps, all seven fields incl. vorticity; every initial condition; and
+the API-behaviour quirks (max_time cap, run_until step count, p/T/q alternation, PE T/P
+drift, stale grid handle, set_dt, re-initialize). Full-size cases compare SHA-256 digests
+of the reference's outputs (tests/golden/ref_large.json) -- bitwise at BASELINE sizes.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import golden, large_digests
+
+pytestmark = pytest.mark.gpu
+
+ws = pytest.importorskip("weather_sim")
+if not ws.is_cuda_available():  # pragma: no cover - the gpu marker is deselected on CPU
+    pytest.skip("no HIP device", allow_module_level=True)
+
+FIELDS = ("u", "v", "h", "p", "t", "q", "vort")
+
+
+def make_sim(width, height, model, method, fp64, dx=1.0, dy=1.0, dt=0.01, g=9.81, f=0.0, max_time=10.0, levels=1):
+    c = ws.SimulationConfig()
+    c.grid_width, c.grid_height, c.num_levels = width, height, levels
+    c.model, c.integration_method = model, method
+    c.dx, c.dy, c.dt, c.gravity, c.coriolis_f, c.max_time = dx, dy, dt, g, f, max_time
+    c.double_precision = fp64
+    return ws.WeatherSimulation(c)
+
+
+def state(grid, level=None):
+    u, v = grid.get_velocity_field(level)
+    return {"u": u, "v": v, "h": grid.get_height_field(level), "p": grid.get_pressure_field(level),
+            "t": grid.get_temperature_field(level), "q": grid.get_humidity_field(level),
+            "vort": grid.get_vorticity_field(level)}
+
+
+def assert_bitwise(grid, ref, what, fields=FIELDS):
+    got = state(grid)
+    for k in fields:
+        assert got[k].dtype == ref[k].dtype, (what, k)
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{what}: field {k}")
+
+
+def load(sim, s0):
+    sim.initialize()
+    g = sim.get_current_grid()
+    g.set_velocity_field(s0["u"], s0["v"])
+    g.set_height_field(s0["h"])
+    g.set_pressure_field(s0["p"])
+    g.set_temperature_field(s0["t"])
+    g.set_humidity_field(s0["q"])
+
+
+@pytest.mark.parametrize("variant", ["f32", "f64"])
+def test_stepping_bitwise(variant):
+    gold = golden(variant)
+    cases = gold.cases("step/")
+    assert len(cases) >= 20
+    for case in cases:
+        cfg = gold.meta[case]["cfg"]
+        sim = make_sim(cfg["width"], cfg["height"], cfg["model"], cfg["method"], variant == "f64",
+                       dx=cfg.get("dx", 1.0), dy=cfg.get("dy", 1.0), dt=cfg.get("dt", 0.01), g=cfg.get("g", 9.81),
+                       f=cfg.get("f", 0.0))
+        load(sim, gold.snap(case, "s0"))
+        sim.step()
+        for snap, n in (("s1", 0), ("s10", 9), ("s50", 40)):
+            if n:
+                sim.run(n)
+            ref = gold.snap(case, snap)
+            assert sim.get_current_step() == ref["step"]
+            assert sim.get_current_time() == ref["time"]
+            assert_bitwise(sim.get_current_grid(), ref, f"{case} {snap}")
+
+
+@pytest.mark.parametrize("variant", ["f32", "f64"])
+def test_initial_conditions_bitwise(variant):
+    gold = golden(variant)
+    cases = gold.cases("ic/") + gold.cases("ic37x53/")
+    for case in cases:
+        name = case.split("/", 1)[1]
+        W, H = (48, 32) if case.startswith("ic/") else (37, 53)
+        args = {"random": (42, 1.0), "atmospheric_profile_tropical": ("tropical",),
+                "atmospheric_profile_polar": ("polar",), "jet_stream_custom": (0.3, 0.07, 13.5, 9.75),
+                "vortex_custom": (0.4, 0.6, 0.2, 5.0, 11.0)}.get(name, ())
+        base = name.replace("_tropical", "").replace("_polar", "").replace("_custom", "")
+        cls = {"uniform": ws.UniformInitialCondition, "random": ws.RandomInitialCondition,
+               "zonal_flow": ws.ZonalFlowInitialCondition, "vortex": ws.VortexInitialCondition,
+               "jet_stream": ws.JetStreamInitialCondition, "breaking_wave": ws.BreakingWaveInitialCondition,
+               "front": ws.FrontInitialCondition, "mountain": ws.MountainInitialCondition,
+               "atmospheric_profile": ws.AtmosphericProfileInitialCondition}[base]
+        sim = make_sim(W, H, 0, 2, variant == "f64")
+        sim.set_initial_condition(cls(*args))
+        sim.initialize()
+        assert_bitwise(sim.get_current_grid(), gold.snap(case, "s0"), case)
+
+
+@pytest.mark.parametrize("variant", ["f32", "f64"])
+def test_api_behaviour(variant):
+    gold = golden(variant)
+    fp64 = variant == "f64"
+    # run(2000) with max_time = 10 stops at t >= max_time
+    sim = make_sim(16, 12, 0, 0, fp64)
+    sim.set_initial_condition(ws.JetStreamInitialCondition())
+    sim.initialize()
+    ref = gold.snap("api/max_time_cap", "end")
+    assert sim.run(2000) == ref["step"]
+    assert sim.get_current_time() == ref["time"]
+    assert_bitwise(sim.get_current_grid(), ref, "max_time_cap")
+    # run_until
+    sim = make_sim(16, 12, 0, 1, fp64, dt=0.1)
+    sim.set_initial_condition(ws.ZonalFlowInitialCondition())
+    sim.initialize()
+    for snap, t in (("a", 0.5), ("b", 0.55), ("c", 1.25)):
+        sim.run_until(t)
+        ref = gold.snap("api/run_until", snap)
+        assert sim.get_current_step() == ref["step"], snap
+        assert sim.get_current_time() == ref["time"]
+        assert_bitwise(sim.get_current_grid(), ref, f"run_until {snap}")
+    # alternation of p/T/q between the two grids; PE T/P drift
+    for model in (0, 2):
+        sim = make_sim(16, 12, model, 0, fp64)
+        sim.set_initial_condition(ws.UniformInitialCondition(1.0, 0.5, 10.0, 1000.0, 300.0, 0.25))
+        sim.initialize()
+        for snap in "abc":
+            sim.step()
+            assert_bitwise(sim.get_current_grid(), gold.snap(f"api/alternation_m{model}", snap), f"alt m{model} {snap}")
+    # stale handle
+    sim = make_sim(16, 12, 0, 2, fp64)
+    sim.set_initial_condition(ws.BreakingWaveInitialCondition())
+    sim.initialize()
+    sim.step()
+    sim.step()
+    held = sim.get_current_grid()
+    assert_bitwise(held, gold.snap("api/stale_handle", "a"), "stale a")
+    sim.step()
+    assert_bitwise(held, gold.snap("api/stale_handle", "b"), "stale b")
+    assert_bitwise(sim.get_current_grid(), gold.snap("api/stale_handle", "c"), "stale c")
+    sim.step()
+    assert_bitwise(held, gold.snap("api/stale_handle", "d"), "stale d")
+    # set_dt mid-run
+    sim = make_sim(16, 12, 0, 2, fp64)
+    sim.set_initial_condition(ws.JetStreamInitialCondition())
+    sim.initialize()
+    for _ in range(3):
+        sim.step()
+    sim.set_dt(0.02)
+    for _ in range(4):
+        sim.step()
+    ref = gold.snap("api/set_dt", "a")
+    assert sim.get_current_time() == ref["time"]
+    assert_bitwise(sim.get_current_grid(), ref, "set_dt")
+    # re-initialize after stepping
+    sim = make_sim(16, 12, 0, 0, fp64)
+    sim.set_initial_condition(ws.UniformInitialCondition(1.0, 0.5, 10.0, 1000.0, 300.0, 0.25))
+    sim.initialize()
+    sim.run(3)
+    sim.initialize()
+    sim.step()
+    assert_bitwise(sim.get_current_grid(), gold.snap("api/reinit", "a"), "reinit a")
+    sim.step()
+    assert_bitwise(sim.get_current_grid(), gold.snap("api/reinit", "b"), "reinit b")
+
+
+def test_wrapper_snapshots_and_errors():
+    w = ws.WeatherSimulationWrapper(48, 32, integration_method="rk4", output_interval=5)
+    w.set_initial_condition("breaking_wave")
+    for _ in range(10):
+        w.step()
+    out = w.get_output_data()
+    assert [o["step"] for o in out] == [5, 10]
+    ref = golden("f32").snap("step/m0_i2_breaking_wave", "s10")
+    np.testing.assert_array_equal(out[1]["u"], ref["u"])
+    np.testing.assert_array_equal(out[1]["vorticity"], ref["vort"])
+    g = w.get_grid()
+    with pytest.raises(RuntimeError):
+        g.set_height_field(np.zeros((3, 3), np.float32))
+    with pytest.raises(RuntimeError):
+        g.set_height_field(np.zeros(48 * 32, np.float32))
+    with pytest.raises(ValueError):
+        g.set_spacing(0.0, 1.0)
+    with pytest.raises(ValueError):
+        ws.WeatherGrid(0, 10)
+    m = w.get_metrics()
+    assert m.num_steps == 10 and m.compute_time_ms > 0
+
+
+def test_adapter_and_raw_kernel_abi():
+    gold = golden("f32")
+    s0 = gold.snap("step/m0_i0_jet_stream", "s0")
+    s1 = gold.snap("step/m0_i0_jet_stream", "s1")
+    a = ws.KernelAdapterFactory.get_instance().get_best_adapter()
+    assert a.get_name() == "HIPAdapter"
+    gin, gout = ws.WeatherGrid(48, 32), ws.WeatherGrid(48, 32)
+    gin.set_velocity_field(s0["u"], s0["v"])
+    gin.set_height_field(s0["h"])
+    ms = a.execute_shallow_water_step(gin, gout, 0.01)
+    assert ms >= 0
+    u, v = gout.get_velocity_field()
+    np.testing.assert_array_equal(u, s1["u"])
+    np.testing.assert_array_equal(v, s1["v"])
+    np.testing.assert_array_equal(gout.get_height_field(), s1["h"])
+    np.testing.assert_array_equal(gout.get_vorticity_field(), s1["vort"])
+
+
+def _digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _dam_break(W, H, width_cells, dtype):
+    x = np.arange(W, dtype=np.float64)
+    row = 10.0 + 0.5 * (1.0 - np.tanh((x - W / 2) / width_cells))
+    return np.broadcast_to(row, (H, W)).astype(dtype)
+
+
+@pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
+                                  "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
+                                  "C3_zonal_flow_2048_baro_f32"])
+def test_full_size_digests(name):
+    d = large_digests()[name]
+    spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
+    W, H = int(spec["width"]), int(spec["height"])
+    fp64 = d["variant"] == "f64"
+    sim = make_sim(W, H, int(spec["model"]), int(spec["method"]), fp64, max_time=float(spec["max_time"]))
+    ic = [l for l in d["spec"] if l.startswith("ic ")]
+    if ic:
+        name_ic = ic[0].split()[1]
+        sim.set_initial_condition({"jet_stream": ws.JetStreamInitialCondition,
+                                   "zonal_flow": ws.ZonalFlowInitialCondition}[name_ic]())
+    sim.initialize()
+    if not ic:
+        sim.get_current_grid().set_height_field(_dam_break(W, H, 8.0 if W == 256 else 128.0,
+                                                           np.float64 if fp64 else np.float32))
+    steps = int([l for l in d["spec"] if l.startswith("run ")][0].split()[1])
+    assert sim.run(steps) == d["step"]
+    g = sim.get_current_grid()
+    got = state(g)
+    for k, h in d["sha256"].items():
+        if _digest(got[k]) != h:
+            ref_l2 = d["l2"][k]
+            pytest.fail(f"{name}: {k} digest mismatch (|got|={np.linalg.norm(got[k].astype(np.float64))!r} "
+                        f"|ref|={ref_l2!r})")
+
+
+def test_pe_levels_match_reference_per_level():
+    """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
+    must equal a standalone reference run of that level (bitwise)."""
+    digests = large_digests()
+    L = 32
+    sim = make_sim(1024, 1024, 2, 2, False, max_time=1e30, levels=L)
+    sim.initialize()
+    g = sim.get_current_grid()
+    for k in range(L):
+        ws.JetStreamInitialCondition(0.5, 0.1, 10.0 * (1.0 + k / 32.0), 10.0).initialize(g, level=k)
+    sim.run(10)
+    g = sim.get_current_grid()
+    for k in (0, 7, 31):
+        d = digests[f"C4_pe_1024_level{k}_f32"]
+        got = state(g, level=k)
+        for f, h in d["sha256"].items():
+            assert _digest(got[f]) == h, (k, f)
