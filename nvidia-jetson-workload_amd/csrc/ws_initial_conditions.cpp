@@ -18,6 +18,12 @@
 namespace ws {
 namespace {
 
+// The reference build (g++ -O3) fuses a sin and a cos of the same argument into one libm
+// sincos / sincosf call (its .so imports sincos@GLIBC, no cos); glibc's sincos can differ
+// from cos by 1 ulp, so the fused call is reproduced explicitly.
+inline void ref_sincos(double x, double* s, double* c) { ::sincos(x, s, c); }
+inline void ref_sincos(float x, float* s, float* c) { ::sincosf(x, s, c); }
+
 // setParameter(name, scalar_t value) -> std::to_string; getParameter<float> -> std::stof
 template <typename T>
 float param_roundtrip(double v) {
@@ -135,9 +141,11 @@ void breaking_wave(IcFields<T>& f, const P<T>& a) {
         for (int x = 0; x < f.W; ++x) {
             const T wave_phase = wave_k * x - 0.1f * y_norm;
             const T wave_amp = amplitude * std::exp(-std::pow(y_norm - 0.5f, 2) / 0.05f);
-            const T u = u_base + wave_amp * std::sin(wave_phase);
-            const T v = wave_amp * std::cos(wave_phase);
-            const T h = h_mean + wave_amp * std::cos(wave_phase);
+            T sn, cs;
+            ref_sincos(wave_phase, &sn, &cs);
+            const T u = u_base + wave_amp * sn;
+            const T v = wave_amp * cs;
+            const T h = h_mean + wave_amp * cs;
             const size_t i = f.idx(x, y);
             f.u[i] = u; f.v[i] = v; f.h[i] = h;
         }
@@ -240,8 +248,10 @@ void atmospheric_profile(IcFields<T>& f, const std::string& profile_name) {
         const T t_base = pr.t[idx], p_base = pr.p[idx], q_base = pr.q[idx], u_base = pr.u[idx], v_base = pr.v[idx];
         for (int x = 0; x < f.W; ++x) {
             const T x_norm = static_cast<T>(x) / (f.W - 1);
-            const T t_var = 2.0f * std::sin(2.0f * M_PI * x_norm);
-            const T p_var = 2.0f * std::cos(2.0f * M_PI * x_norm);
+            double sn, cs;
+            ref_sincos(2.0f * M_PI * x_norm, &sn, &cs);
+            const T t_var = 2.0f * sn;
+            const T p_var = 2.0f * cs;
             const T q_var = 0.02f * std::sin(4.0f * M_PI * x_norm);
             const size_t i = f.idx(x, y);
             f.t[i] = t_base + t_var;
