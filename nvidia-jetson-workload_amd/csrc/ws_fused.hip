@@ -1,0 +1,275 @@
+// Fused multi-stage time step: one kernel per time step (Euler: 1 stage, RK2: 2, RK4: 4).
+//
+// Why: the unfused stage kernels move 6w / 15w / 45w bytes per cell per step (Euler /
+// RK2 / RK4-as-implemented); this kernel moves ~6w for every integrator --
+// y = (u, v, h) is read once and y' written once -- and keeps every intermediate stage
+// (tmp, K2, K3) on chip. Arithmetic per cell is identical to the reference, in the same
+// order (weather_simulation.cpp:160-218, 220-323, 325-455, 473-540), so results stay
+// bit-for-bit equal to the CPU solver; redundantly recomputed halo cells are discarded.
+//
+// Decomposition (CDNA4): a workgroup of kFusedCols lanes owns a column strip (one column
+// per lane) and marches down a segment of rows. At march step R it takes input row R
+// (loaded kPf rows ahead into registers) and stage s = 1..NST computes row R - s (a skewed
+// wavefront). Vertical neighbours come from per-lane register rings; horizontal neighbours
+// come from the LDS copy of the previous stage's row, published one march step earlier, so
+// the whole pipeline needs ONE workgroup barrier per row. Each stage invalidates one column
+// at each strip edge: a strip outputs kFusedCols - 2*NST columns and neighbouring strips
+// overlap by 2*NST columns. A segment of S output rows marches S + 2*NST rows (warm-up +
+// drain), rounded up to the unroll length.
+#include <type_traits>
+
+#include "ws_fused.h"
+
+namespace ws {
+namespace {
+
+template <typename T>
+struct V3 {
+    T u, v, h;
+};
+
+// (a_r - a_l) / (2 d). POW2 (every 2dx, 2dy a power of two): the exact reciprocal gives the
+// same correctly rounded quotient; otherwise the IEEE divide.
+template <bool POW2, typename T>
+__device__ __forceinline__ T cdiff(T ar, T al, T two_d, T inv) {
+    if constexpr (POW2) return (ar - al) * inv;
+    else return (ar - al) / two_d;
+}
+
+// SWE tendency (weather_simulation.cpp:521-537), same evaluation order.
+template <bool POW2, typename T>
+__device__ __forceinline__ V3<T> tend(const V3<T>& c, const V3<T>& l, const V3<T>& r, const V3<T>& t,
+                                      const V3<T>& b, const Spacing<T>& sp, T g, T f) {
+    const T u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
+    const T u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
+    const T v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
+    const T v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
+    const T h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
+    const T h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
+    V3<T> k;
+    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
+    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
+    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
+    return k;
+}
+
+template <typename T>
+__device__ __forceinline__ V3<T> axpy(const V3<T>& y, T c, const V3<T>& k) {
+    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
+}
+
+// LDS image of one published row: [field][1 + column + 1]. Lane c's value sits at c + 1;
+// its neighbours at c and c + 2 (one ds_read2 per field). The reference's clamp-to-self at
+// the global x edges (weather_simulation.cpp:510-511) is done on the WRITE side: the lane
+// at x = 0 also writes its value into its left slot, the lane at x = W-1 into its right
+// slot; lanes outside [0, W) publish into slot 0 (never read by a live output).
+template <typename T>
+struct RowSlot {
+    T f[3][kFusedCols + 2];
+};
+
+template <typename T>
+__device__ __forceinline__ void publish(RowSlot<T>& s, int pub, int pub2, const V3<T>& v) {
+    s.f[0][pub] = v.u;
+    s.f[1][pub] = v.v;
+    s.f[2][pub] = v.h;
+    s.f[0][pub2] = v.u;  // clamp copy (== pub for interior lanes: a same-value rewrite)
+    s.f[1][pub2] = v.v;
+    s.f[2][pub2] = v.h;
+}
+
+// One stage at row j: the tendency of (prev stage) at row j from rows j-1 (up), j (mid),
+// j+1 (down) and the published row j (x-neighbours). YCLAMP: the segment touches a
+// global y edge, where the reference clamps j-1 / j+1 to j (weather_simulation.cpp:512-513).
+template <bool POW2, bool YCLAMP, typename T>
+__device__ __forceinline__ V3<T> stage_tend(const RowSlot<T>& pub, int lane, int j, const Geom& g, const V3<T>& up,
+                                            const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav, T cor) {
+    const V3<T> l{pub.f[0][lane], pub.f[1][lane], pub.f[2][lane]};
+    const V3<T> r{pub.f[0][lane + 2], pub.f[1][lane + 2], pub.f[2][lane + 2]};
+    if constexpr (YCLAMP) {
+        const bool ytop = (j == 0) && g.top_clamp;
+        const bool ybot = (j == g.H - 1) && g.bot_clamp;
+        // select by value (a ?: on two lvalues selects an address and spills to scratch)
+        const V3<T> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
+        const V3<T> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
+        return tend<POW2>(mid, l, r, t, b, sp, grav, cor);
+    } else {
+        return tend<POW2>(mid, l, r, up, down, sp, grav, cor);
+    }
+}
+
+constexpr int kPf = 3;  // rows of y loads in flight per lane
+constexpr int kU = 8;   // march unroll = y ring length
+
+template <typename T, int NST>
+struct March {
+    static constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
+    static_assert(kYb + kPf <= kU, "y ring too short");
+
+    V3<T> Y[kU];                // Y[r % kU] = y row r (rows R-kYb+1 .. R+kPf live)
+    V3<T> S1[2], S2[2], S3[2];  // S[r % 2] = stage output at row r
+    V3<T> K2[2], K3[2];         // RK4 stage-2 / stage-3 tendencies, [r % 2] = row r
+};
+
+#ifndef WS_FUSED_MINW
+#define WS_FUSED_MINW 1
+#endif
+
+template <typename T, int NST, bool POW2>
+__global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(FusedArgs<T> a, Geom g) {
+    // All per-lane state lives in rotating register rings indexed by the march phase P
+    // (compile-time): the body is instantiated for P = 0..kU-1, so ring "shifts" are renames,
+    // not moves (hipcc will not runtime-unroll a loop that contains a barrier).
+    __shared__ RowSlot<T> lds[NST][2];  // published rows of stage 0 (= y) .. NST-1
+
+    const int lane = threadIdx.x;
+    const int out_w = kFusedCols - 2 * NST;
+    const int x = blockIdx.x * out_w - NST + lane;  // this lane's global column
+    const bool xlive = x >= 0 && x < g.W;
+    const bool xout = xlive && lane >= NST && lane < kFusedCols - NST;
+    const int pub = xlive ? lane + 1 : 0;
+    const int pub2 = x == 0 ? lane : (x == g.W - 1 ? lane + 2 : pub);
+
+    const int y0 = blockIdx.y * a.seg_rows;
+    const int y1 = min(y0 + a.seg_rows, g.H);
+    const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + NST;
+
+    const int64_t lofs = (int64_t)blockIdx.z * g.lstride;
+    const T* __restrict__ iu = a.in_u + lofs;
+    const T* __restrict__ iv = a.in_v + lofs;
+    const T* __restrict__ ih = a.in_h + lofs;
+    T* __restrict__ ou = a.out_u + lofs;
+    T* __restrict__ ov = a.out_v + lofs;
+    T* __restrict__ oh = a.out_h + lofs;
+
+    // Always-issued loads at clamped (allocated) addresses: dead rows / columns hold real
+    // data that no live output reads, and no branch splits the load stream.
+    const int xc = min(max(x, 0), g.W - 1);
+    auto load_row = [&](int R) -> V3<T> {
+        const int r = min(max(R, row_lo), row_hi - 1);
+        const int64_t i = (int64_t)r * g.pitch + xc;
+        return V3<T>{iu[i], iv[i], ih[i]};
+    };
+    auto store_row = [&](int j, const V3<T>& o) {
+        if (xout && j >= y0 && j < y1) {
+            const int64_t i = (int64_t)j * g.pitch + x;
+            __builtin_nontemporal_store(o.u, ou + i);
+            __builtin_nontemporal_store(o.v, ov + i);
+            __builtin_nontemporal_store(o.h, oh + i);
+        }
+    };
+
+    March<T, NST> m;
+    const V3<T> Z{T(0), T(0), T(0)};
+#pragma unroll
+    for (int i = 0; i < kU; ++i) m.Y[i] = Z;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) m.S1[i] = m.S2[i] = m.S3[i] = m.K2[i] = m.K3[i] = Z;
+
+    // march rows [R0, R1), R1 - R0 rounded up to kU (extra rows: clamped loads, no stores)
+    const int R0 = y0 - NST;
+    const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;
+#pragma unroll
+    for (int i = 0; i < kPf; ++i) m.Y[i] = load_row(R0 + i);
+
+    auto body = [&](auto Pc, auto Cc, int R) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr bool YC = decltype(Cc)::value;
+        constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
+        constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
+        const int cur = R & 1, prv = cur ^ 1;
+        m.Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        publish(lds[0][cur], pub, pub2, m.Y[yi(0)]);
+
+        // stage 1 at row R-1 from y rows R-2, R-1, R
+        const V3<T> k1 = stage_tend<POW2, YC>(lds[0][prv], lane, R - 1, g, m.Y[yi(-2)], m.Y[yi(-1)], m.Y[yi(0)],
+                                              a.sp1, a.gravity, a.coriolis_f);
+        if constexpr (NST == 1) {
+            store_row(R - 1, axpy(m.Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
+        } else {
+            const V3<T> s1 = axpy(m.Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+            // stage 2 at row R-2 from s1 rows R-3, R-2, R-1
+            const V3<T> k2 = stage_tend<POW2, YC>(lds[1][prv], lane, R - 2, g, m.S1[r2(-3)], m.S1[r2(-2)], s1,
+                                                  a.sp2, a.gravity, a.coriolis_f);
+            publish(lds[1][cur], pub, pub2, s1);
+            m.S1[r2(-1)] = s1;
+            if constexpr (NST == 2) {
+                store_row(R - 2, axpy(m.Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+            } else {
+                const V3<T> s2 = axpy(m.Y[yi(-2)], a.c_half, k2);
+                // stage 3 at row R-3
+                const V3<T> k3 = stage_tend<POW2, YC>(lds[2][prv], lane, R - 3, g, m.S2[r2(-4)], m.S2[r2(-3)], s2,
+                                                      a.sp2, a.gravity, a.coriolis_f);
+                const V3<T> s3 = axpy(m.Y[yi(-3)], a.c_dt, k3);
+                // stage 4 at row R-4
+                const V3<T> k4 = stage_tend<POW2, YC>(lds[3][prv], lane, R - 4, g, m.S3[r2(-5)], m.S3[r2(-4)], s3,
+                                                      a.sp2, a.gravity, a.coriolis_f);
+                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                const T two = T(2);
+                const V3<T>& y4 = m.Y[yi(-4)];
+                const V3<T>& kk2 = m.K2[r2(-4)];
+                const V3<T>& kk3 = m.K3[r2(-4)];
+                V3<T> o;
+                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
+                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
+                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                store_row(R - 4, o);
+                publish(lds[2][cur], pub, pub2, s2);
+                publish(lds[3][cur], pub, pub2, s3);
+                m.S2[r2(-2)] = s2;
+                m.S3[r2(-3)] = s3;
+                m.K2[r2(-2)] = k2;
+                m.K3[r2(-3)] = k3;
+            }
+        }
+        __syncthreads();
+    };
+
+    auto march = [&](auto Cc) {
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        using I4 = std::integral_constant<int, 4>;
+        using I5 = std::integral_constant<int, 5>;
+        using I6 = std::integral_constant<int, 6>;
+        using I7 = std::integral_constant<int, 7>;
+        for (int R = R0; R < R1; R += kU) {
+            body(I0{}, Cc, R); body(I1{}, Cc, R + 1); body(I2{}, Cc, R + 2); body(I3{}, Cc, R + 3);
+            body(I4{}, Cc, R + 4); body(I5{}, Cc, R + 5); body(I6{}, Cc, R + 6); body(I7{}, Cc, R + 7);
+        }
+    };
+    // Rows j == 0 / j == H-1 (clamped) feed live outputs only in segments within NST rows
+    // of the global top / bottom edge; every other segment runs the clamp-free body.
+    const bool yclamp = (g.top_clamp && y0 < NST) || (g.bot_clamp && y1 > g.H - NST);
+    if (yclamp) march(std::true_type{});
+    else march(std::false_type{});
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
+    if (g.W < 2) return hipErrorInvalidValue;  // x = 0 == W-1 needs two clamp copies: use the stage kernels
+    const int out_w = kFusedCols - 2 * nstages;
+    const dim3 grid((g.W + out_w - 1) / out_w, (g.H + a.seg_rows - 1) / a.seg_rows, g.L);
+    const dim3 block(kFusedCols);
+    const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
+#define WS_FUSED_LAUNCH(N)                                                                               \
+    if (pow2) hipLaunchKernelGGL((fused_step_kernel<T, N, true>), grid, block, 0, s, a, g);              \
+    else hipLaunchKernelGGL((fused_step_kernel<T, N, false>), grid, block, 0, s, a, g);
+    switch (nstages) {
+        case 1: WS_FUSED_LAUNCH(1) break;
+        case 2: WS_FUSED_LAUNCH(2) break;
+        case 4: WS_FUSED_LAUNCH(4) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef WS_FUSED_LAUNCH
+    return hipGetLastError();
+}
+
+template hipError_t launch_fused_step<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t);
+template hipError_t launch_fused_step<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t);
+
+}  // namespace ws

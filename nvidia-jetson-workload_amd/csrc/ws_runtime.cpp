@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <stdexcept>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "ws_comm.h"
+#include "ws_fused.h"
 #include "ws_ic.h"
 #include "ws_internal.h"
 #include "ws_timer.h"
@@ -217,9 +219,25 @@ struct ws_sim {
     double last_ms = 0.0;
     int64_t last_launches = 0;
     ws::KernelTimer timer;
+    bool fused = true;        // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
+    int32_t seg_override = 0; // WS_SEG_ROWS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
     int32_t row0 = 0;
+
+    // Rows per fused-kernel segment: enough workgroups for ~2 per CU (256 CUs), but
+    // segments long enough that the 2*NST warm-up rows stay a small overhead.
+    int32_t seg_rows(int nst) const {
+        if (seg_override > 0) return seg_override;
+        const ws_grid* g = slot[0];
+        const int out_w = ws::kFusedCols - 2 * nst;
+        const int64_t strips = (g->W + out_w - 1) / out_w;
+        const int64_t want_segs = std::max<int64_t>(1, (512 + strips * g->L - 1) / (strips * g->L));
+        int64_t rows = (g->H + want_segs - 1) / want_segs;
+        rows = std::max<int64_t>(rows, 24 * nst);
+        rows = (rows + 2 * nst + 7) / 8 * 8 - 2 * nst;  // march length (rows + 2 NST) a multiple of the unroll
+        return (int32_t)std::max<int64_t>(1, std::min<int64_t>(rows, g->H));
+    }
 };
 
 namespace {
@@ -264,7 +282,27 @@ void enqueue_step(ws_sim* s) {
     const T dt = (T)s->dt;
     const T half = T(0.5f) * dt;  // `0.5f * dt_` (weather_simulation.cpp:249)
     const int method = effective_method(s->cfg);
-    if (method == WS_EULER) {
+    if (s->fused && c->W >= 2) {
+        // one kernel per step: all stages on chip, y read once, y' written once (6 words/cell)
+        const int nst = method == WS_EULER ? 1 : method == WS_RK2 ? 2 : 4;
+        const ws::Geom g = c->geom();
+        if (s->comm) s->comm->exchange(c->f, 3, (int)sizeof(T), g, nst, s->stream);
+        ws::FusedArgs<T> a{};
+        a.in_u = (const T*)c->f[0]; a.in_v = (const T*)c->f[1]; a.in_h = (const T*)c->f[2];
+        a.out_u = (T*)n->f[0]; a.out_v = (T*)n->f[1]; a.out_h = (T*)n->f[2];
+        a.c_half = half;
+        a.c_dt = dt;
+        a.c_dt6 = dt / T(6.0f);
+        a.gravity = (T)s->cfg.gravity;
+        a.coriolis_f = (T)s->cfg.coriolis_f;
+        a.sp1 = make_spacing<T>(c->dx, c->dy);
+        a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
+        a.seg_rows = s->seg_rows(nst);
+        s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L, s->stream);
+        WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, s->stream));
+        s->timer.end(s->stream);
+        ++s->last_launches;
+    } else if (method == WS_EULER) {
         launch<T>(s, ws::kAxpy, stage_args<T>(c, c, n, dt, s), c, 0, 6);
     } else if (method == WS_RK2) {
         launch<T>(s, ws::kAxpy, stage_args<T>(c, c, s->tmpA, half, s), c, 0, 6);
@@ -365,9 +403,11 @@ ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm
         WS_HIP_CHECK(hipEventCreate(&s->ev1));
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
+        if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
+        if (const char* e = std::getenv("WS_SEG_ROWS")) s->seg_override = std::atoi(e);
         const int method = effective_method(*cfg);
-        if (method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
-        if (method == WS_RK4) {
+        if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
+        if (!s->fused && method == WS_RK4) {
             s->tmpB = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
             s->K2 = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
             s->K3 = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);

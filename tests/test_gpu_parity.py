@@ -56,8 +56,10 @@ def load(sim, s0):
     g.set_humidity_field(s0["q"])
 
 
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused_step_kernel", "stage_kernels"])
 @pytest.mark.parametrize("variant", ["f32", "f64"])
-def test_stepping_bitwise(variant):
+def test_stepping_bitwise(variant, fused, monkeypatch):
+    monkeypatch.setenv("WS_FUSED", fused)
     gold = golden(variant)
     cases = gold.cases("step/")
     assert len(cases) >= 20
@@ -263,3 +265,51 @@ def test_pe_levels_match_reference_per_level():
         got = state(g, level=k)
         for f, h in d["sha256"].items():
             assert _digest(got[f]) == h, (k, f)
+
+
+@pytest.mark.parametrize("seg_rows", ["0", "5", "33"])
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_fused_tiling_vs_oracle(fp64, method, seg_rows, monkeypatch):
+    """Strip (x) and segment (y) seams of the fused kernel: 700 x 77 grid spans three
+    256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle."""
+    from oracle.ws_oracle import OracleSim
+
+    monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
+    W, H = 700, 77
+    sim = make_sim(W, H, 0, method, fp64, dx=1.0, dy=2.0, f=0.3)
+    sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
+    sim.initialize()
+    g = sim.get_current_grid()
+    ref = OracleSim(W, H, 0, method, dx=1.0, dy=2.0, coriolis_f=0.3, precision="f64" if fp64 else "f32")
+    ref.initialize()
+    u, v = g.get_velocity_field()
+    for k, a in (("u", u), ("v", v), ("h", g.get_height_field())):
+        ref.set_field(k, a)
+    sim.run(6)
+    ref.run(6)
+    g = sim.get_current_grid()
+    got = state(g)
+    for k in ("u", "v", "h", "vort"):
+        np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
+
+
+def test_fused_non_pow2_spacing_vs_oracle():
+    """dx = 0.75: 2dx is not a power of two -> the IEEE-divide instantiation."""
+    from oracle.ws_oracle import OracleSim
+
+    W, H = 300, 40
+    sim = make_sim(W, H, 0, 2, False, dx=0.75, dy=1.3)
+    sim.set_initial_condition(ws.VortexInitialCondition(0.5, 0.5, 0.3, 3.0, 10.0))
+    sim.initialize()
+    g = sim.get_current_grid()
+    ref = OracleSim(W, H, 0, 2, dx=0.75, dy=1.3)
+    ref.initialize()
+    u, v = g.get_velocity_field()
+    for k, a in (("u", u), ("v", v), ("h", g.get_height_field())):
+        ref.set_field(k, a)
+    sim.run(4)
+    ref.run(4)
+    got = state(sim.get_current_grid())
+    for k in ("u", "v", "h", "vort"):
+        np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
