@@ -21,7 +21,12 @@ struct FusedArgs {
 };
 
 // nstages: 1 (Euler), 2 (RK2 midpoint), 4 (RK4-as-implemented)
+// LDS variant: 256-lane workgroups, horizontal neighbours through LDS, one barrier per row.
 template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+// DPP variant: independent 64-lane waves, horizontal neighbours by DPP lane shifts.
+constexpr int kDppCols = 64;
+template <typename T>
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
 }  // namespace ws

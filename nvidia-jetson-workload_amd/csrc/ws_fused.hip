@@ -17,6 +17,7 @@
 // overlap by 2*NST columns. A segment of S output rows marches S + 2*NST rows (warm-up +
 // drain), rounded up to the unroll length.
 #include <type_traits>
+#include <utility>
 
 #include "ws_fused.h"
 
@@ -58,34 +59,43 @@ __device__ __forceinline__ V3<T> axpy(const V3<T>& y, T c, const V3<T>& k) {
     return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
 }
 
-// LDS image of one published row: [field][1 + column + 1]. Lane c's value sits at c + 1;
-// its neighbours at c and c + 2 (one ds_read2 per field). The reference's clamp-to-self at
-// the global x edges (weather_simulation.cpp:510-511) is done on the WRITE side: the lane
-// at x = 0 also writes its value into its left slot, the lane at x = W-1 into its right
-// slot; lanes outside [0, W) publish into slot 0 (never read by a live output).
-template <typename T>
-struct RowSlot {
-    T f[3][kFusedCols + 2];
+// LDS image, column-major: column c (= lane + 1; columns 0 and kFusedCols + 1 are pads)
+// holds, for every published quantity q = 2 * stage + (row parity), the three fields at
+// [c][q][field]. The column stride kCs = 6*NST + 1 elements (odd in dwords for fp32,
+// 2 mod 4 for fp64) spreads the 32 / 64 lanes of one access over distinct banks, and a
+// lane's left and right neighbours (columns lane, lane + 2) sit within one ds_read2's
+// offset range of a single per-lane base address, so every LDS access uses one address
+// register plus immediate offsets.
+//
+// Clamp-to-self at the global x edges (weather_simulation.cpp:510-511) is done on the
+// WRITE side (XCLAMP strips only): the lane at x = 0 also writes its value into its left
+// column, the lane at x = W-1 into its right column, and lanes outside [0, W) publish
+// into pad column 0 (never read by a live output).
+template <typename T, int NST>
+struct Lds {
+    static constexpr int kCs = 6 * NST + 1;
+    T a[(kFusedCols + 2) * kCs];
+    __device__ __forceinline__ T* col(int c) { return a + c * kCs; }
 };
 
-template <typename T>
-__device__ __forceinline__ void publish(RowSlot<T>& s, int pub, int pub2, const V3<T>& v) {
-    s.f[0][pub] = v.u;
-    s.f[1][pub] = v.v;
-    s.f[2][pub] = v.h;
-    s.f[0][pub2] = v.u;  // clamp copy (== pub for interior lanes: a same-value rewrite)
-    s.f[1][pub2] = v.v;
-    s.f[2][pub2] = v.h;
+template <int NST, int Q, typename T>
+__device__ __forceinline__ void publish(T* colp, const V3<T>& v) {
+    colp[Q * 3 + 0] = v.u;
+    colp[Q * 3 + 1] = v.v;
+    colp[Q * 3 + 2] = v.h;
 }
 
 // One stage at row j: the tendency of (prev stage) at row j from rows j-1 (up), j (mid),
-// j+1 (down) and the published row j (x-neighbours). YCLAMP: the segment touches a
-// global y edge, where the reference clamps j-1 / j+1 to j (weather_simulation.cpp:512-513).
-template <bool POW2, bool YCLAMP, typename T>
-__device__ __forceinline__ V3<T> stage_tend(const RowSlot<T>& pub, int lane, int j, const Geom& g, const V3<T>& up,
-                                            const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav, T cor) {
-    const V3<T> l{pub.f[0][lane], pub.f[1][lane], pub.f[2][lane]};
-    const V3<T> r{pub.f[0][lane + 2], pub.f[1][lane + 2], pub.f[2][lane + 2]};
+// j+1 (down) and the published row j (x-neighbours, quantity Q). YCLAMP: the segment
+// touches a global y edge, where the reference clamps j-1 / j+1 to j
+// (weather_simulation.cpp:512-513).
+template <bool POW2, bool YCLAMP, int NST, int Q, typename T>
+__device__ __forceinline__ V3<T> stage_tend(const T* lcol, int j, const Geom& g, const V3<T>& up, const V3<T>& mid,
+                                            const V3<T>& down, const Spacing<T>& sp, T grav, T cor) {
+    constexpr int kCs = Lds<T, NST>::kCs;
+    const T* rcol = lcol + 2 * kCs;
+    const V3<T> l{lcol[Q * 3 + 0], lcol[Q * 3 + 1], lcol[Q * 3 + 2]};
+    const V3<T> r{rcol[Q * 3 + 0], rcol[Q * 3 + 1], rcol[Q * 3 + 2]};
     if constexpr (YCLAMP) {
         const bool ytop = (j == 0) && g.top_clamp;
         const bool ybot = (j == g.H - 1) && g.bot_clamp;
@@ -101,16 +111,6 @@ __device__ __forceinline__ V3<T> stage_tend(const RowSlot<T>& pub, int lane, int
 constexpr int kPf = 3;  // rows of y loads in flight per lane
 constexpr int kU = 8;   // march unroll = y ring length
 
-template <typename T, int NST>
-struct March {
-    static constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
-    static_assert(kYb + kPf <= kU, "y ring too short");
-
-    V3<T> Y[kU];                // Y[r % kU] = y row r (rows R-kYb+1 .. R+kPf live)
-    V3<T> S1[2], S2[2], S3[2];  // S[r % 2] = stage output at row r
-    V3<T> K2[2], K3[2];         // RK4 stage-2 / stage-3 tendencies, [r % 2] = row r
-};
-
 #ifndef WS_FUSED_MINW
 #define WS_FUSED_MINW 1
 #endif
@@ -119,16 +119,20 @@ template <typename T, int NST, bool POW2>
 __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(FusedArgs<T> a, Geom g) {
     // All per-lane state lives in rotating register rings indexed by the march phase P
     // (compile-time): the body is instantiated for P = 0..kU-1, so ring "shifts" are renames,
-    // not moves (hipcc will not runtime-unroll a loop that contains a barrier).
-    __shared__ RowSlot<T> lds[NST][2];  // published rows of stage 0 (= y) .. NST-1
+    // not moves (hipcc will not runtime-unroll a loop that contains a barrier). The march
+    // starts on an even row, so the LDS double-buffer parity is compile-time too.
+    constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
+    static_assert(kYb + kPf <= kU, "y ring too short");
+    __shared__ Lds<T, NST> lds;
 
     const int lane = threadIdx.x;
     const int out_w = kFusedCols - 2 * NST;
     const int x = blockIdx.x * out_w - NST + lane;  // this lane's global column
     const bool xlive = x >= 0 && x < g.W;
     const bool xout = xlive && lane >= NST && lane < kFusedCols - NST;
-    const int pub = xlive ? lane + 1 : 0;
-    const int pub2 = x == 0 ? lane : (x == g.W - 1 ? lane + 2 : pub);
+    T* const mycol = lds.col(xlive ? lane + 1 : 0);
+    T* const clampcol = lds.col(x == 0 ? lane : (x == g.W - 1 ? lane + 2 : (xlive ? lane + 1 : 0)));
+    const T* const lcol = lds.col(lane);  // left neighbour column; right = lcol + 2 kCs
 
     const int y0 = blockIdx.y * a.seg_rows;
     const int y1 = min(y0 + a.seg_rows, g.H);
@@ -160,91 +164,103 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
         }
     };
 
-    March<T, NST> m;
+    V3<T> Y[kU];                // Y[r % kU] = y row r (rows R-kYb+1 .. R+kPf live)
+    V3<T> S1[2], S2[2], S3[2];  // [r % 2] = stage output at row r
+    V3<T> K2[2], K3[2];         // RK4 stage-2 / stage-3 tendencies at row r
     const V3<T> Z{T(0), T(0), T(0)};
 #pragma unroll
-    for (int i = 0; i < kU; ++i) m.Y[i] = Z;
+    for (int i = 0; i < kU; ++i) Y[i] = Z;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) m.S1[i] = m.S2[i] = m.S3[i] = m.K2[i] = m.K3[i] = Z;
+    for (int i = 0; i < 2; ++i) S1[i] = S2[i] = S3[i] = K2[i] = K3[i] = Z;
 
-    // march rows [R0, R1), R1 - R0 rounded up to kU (extra rows: clamped loads, no stores)
-    const int R0 = y0 - NST;
+    // march rows [R0, R1): R0 even (one dead warm-up row if needed), length a multiple of kU
+    const int R0 = (y0 - NST) & ~1;
     const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;
 #pragma unroll
-    for (int i = 0; i < kPf; ++i) m.Y[i] = load_row(R0 + i);
+    for (int i = 0; i < kPf; ++i) Y[i] = load_row(R0 + i);
 
-    auto body = [&](auto Pc, auto Cc, int R) {
+    auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
         constexpr int P = decltype(Pc)::value;
-        constexpr bool YC = decltype(Cc)::value;
+        constexpr bool XC = decltype(Xc)::value;
+        constexpr bool YC = decltype(Yc)::value;
+        constexpr int cur = P & 1, prv = cur ^ 1;  // R0 even => parity of R is parity of P
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
-        const int cur = R & 1, prv = cur ^ 1;
-        m.Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
-        publish(lds[0][cur], pub, pub2, m.Y[yi(0)]);
+        auto pub = [&](auto Qc, const V3<T>& v) {
+            constexpr int Q = decltype(Qc)::value;
+            publish<NST, Q>(mycol, v);
+            if constexpr (XC) publish<NST, Q>(clampcol, v);
+        };
+        using Q0c = std::integral_constant<int, 0 + cur>;
+        using Q1c = std::integral_constant<int, 2 + cur>;
+        using Q2c = std::integral_constant<int, 4 + cur>;
+        using Q3c = std::integral_constant<int, 6 + cur>;
+
+        Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        pub(Q0c{}, Y[yi(0)]);
 
         // stage 1 at row R-1 from y rows R-2, R-1, R
-        const V3<T> k1 = stage_tend<POW2, YC>(lds[0][prv], lane, R - 1, g, m.Y[yi(-2)], m.Y[yi(-1)], m.Y[yi(0)],
-                                              a.sp1, a.gravity, a.coriolis_f);
+        const V3<T> k1 = stage_tend<POW2, YC, NST, 0 + prv>(lcol, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1,
+                                                            a.gravity, a.coriolis_f);
         if constexpr (NST == 1) {
-            store_row(R - 1, axpy(m.Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
+            store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
         } else {
-            const V3<T> s1 = axpy(m.Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+            const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
             // stage 2 at row R-2 from s1 rows R-3, R-2, R-1
-            const V3<T> k2 = stage_tend<POW2, YC>(lds[1][prv], lane, R - 2, g, m.S1[r2(-3)], m.S1[r2(-2)], s1,
-                                                  a.sp2, a.gravity, a.coriolis_f);
-            publish(lds[1][cur], pub, pub2, s1);
-            m.S1[r2(-1)] = s1;
+            const V3<T> k2 = stage_tend<POW2, YC, NST, 2 + prv>(lcol, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
+                                                                a.gravity, a.coriolis_f);
+            pub(Q1c{}, s1);
+            S1[r2(-1)] = s1;
             if constexpr (NST == 2) {
-                store_row(R - 2, axpy(m.Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+                store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
             } else {
-                const V3<T> s2 = axpy(m.Y[yi(-2)], a.c_half, k2);
+                const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
                 // stage 3 at row R-3
-                const V3<T> k3 = stage_tend<POW2, YC>(lds[2][prv], lane, R - 3, g, m.S2[r2(-4)], m.S2[r2(-3)], s2,
-                                                      a.sp2, a.gravity, a.coriolis_f);
-                const V3<T> s3 = axpy(m.Y[yi(-3)], a.c_dt, k3);
+                const V3<T> k3 = stage_tend<POW2, YC, NST, 4 + prv>(lcol, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2,
+                                                                    a.sp2, a.gravity, a.coriolis_f);
+                const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
                 // stage 4 at row R-4
-                const V3<T> k4 = stage_tend<POW2, YC>(lds[3][prv], lane, R - 4, g, m.S3[r2(-5)], m.S3[r2(-4)], s3,
-                                                      a.sp2, a.gravity, a.coriolis_f);
+                const V3<T> k4 = stage_tend<POW2, YC, NST, 6 + prv>(lcol, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3,
+                                                                    a.sp2, a.gravity, a.coriolis_f);
                 // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
                 const T two = T(2);
-                const V3<T>& y4 = m.Y[yi(-4)];
-                const V3<T>& kk2 = m.K2[r2(-4)];
-                const V3<T>& kk3 = m.K3[r2(-4)];
+                const V3<T>& y4 = Y[yi(-4)];
+                const V3<T>& kk2 = K2[r2(-4)];
+                const V3<T>& kk3 = K3[r2(-4)];
                 V3<T> o;
                 o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
                 o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
                 o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
                 store_row(R - 4, o);
-                publish(lds[2][cur], pub, pub2, s2);
-                publish(lds[3][cur], pub, pub2, s3);
-                m.S2[r2(-2)] = s2;
-                m.S3[r2(-3)] = s3;
-                m.K2[r2(-2)] = k2;
-                m.K3[r2(-3)] = k3;
+                pub(Q2c{}, s2);
+                pub(Q3c{}, s3);
+                S2[r2(-2)] = s2;
+                S3[r2(-3)] = s3;
+                K2[r2(-2)] = k2;
+                K3[r2(-3)] = k3;
             }
         }
         __syncthreads();
     };
 
-    auto march = [&](auto Cc) {
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        using I4 = std::integral_constant<int, 4>;
-        using I5 = std::integral_constant<int, 5>;
-        using I6 = std::integral_constant<int, 6>;
-        using I7 = std::integral_constant<int, 7>;
+    auto march = [&](auto Xc, auto Yc) {
         for (int R = R0; R < R1; R += kU) {
-            body(I0{}, Cc, R); body(I1{}, Cc, R + 1); body(I2{}, Cc, R + 2); body(I3{}, Cc, R + 3);
-            body(I4{}, Cc, R + 4); body(I5{}, Cc, R + 5); body(I6{}, Cc, R + 6); body(I7{}, Cc, R + 7);
+            [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, R + Ps), ...);
+            }(std::make_integer_sequence<int, kU>{});
         }
     };
-    // Rows j == 0 / j == H-1 (clamped) feed live outputs only in segments within NST rows
-    // of the global top / bottom edge; every other segment runs the clamp-free body.
+    // Global edges matter only to strips / segments within NST cells of them; every other
+    // workgroup runs the clamp-free body.
+    const bool xclamp = blockIdx.x == 0 || (int)(blockIdx.x + 1) * out_w >= g.W - NST;
     const bool yclamp = (g.top_clamp && y0 < NST) || (g.bot_clamp && y1 > g.H - NST);
-    if (yclamp) march(std::true_type{});
-    else march(std::false_type{});
+    if (xclamp) {
+        if (yclamp) march(std::true_type{}, std::true_type{});
+        else march(std::true_type{}, std::false_type{});
+    } else {
+        if (yclamp) march(std::false_type{}, std::true_type{});
+        else march(std::false_type{}, std::false_type{});
+    }
 }
 
 }  // namespace

@@ -1,0 +1,274 @@
+// Fused multi-stage time step, wave-independent variant: one 64-lane wave per column strip,
+// horizontal neighbours by DPP lane shifts (wave_shr:1 / wave_shl:1) -- no LDS, no barrier.
+//
+// Same march as ws_fused.hip (one kernel per time step; y read once, y' written once;
+// stage s = 1..NST computes row R - s while row R is taken; register rings indexed by a
+// compile-time phase), but every wave runs free: nothing synchronises it with any other
+// wave, so a wave waiting on HBM never holds its neighbours back. The price is halo
+// redundancy: a 64-column strip outputs 64 - 2*NST columns (RK4: 56, 14% recomputed).
+// Arithmetic per cell is the reference's, in the reference's order
+// (weather_simulation.cpp:160-455, 473-540): results are bit-for-bit those of the CPU solver.
+#include <type_traits>
+
+#include "ws_fused.h"
+
+namespace ws {
+namespace {
+
+constexpr int kWave = 64;
+#ifndef WS_DPP_PF
+#define WS_DPP_PF 3
+#endif
+constexpr int kPf = WS_DPP_PF;             // rows of y loads in flight per lane
+constexpr int kU = (5 + kPf + 1) / 2 * 2;  // march unroll = y ring length (>= 5 past rows + kPf, even)
+
+template <typename T>
+struct V3 {
+    T u, v, h;
+};
+
+// lane i <- lane i-1 (value of the left column) / lane i <- lane i+1 (right column).
+// Lanes without a source keep their own value (edge lanes of a strip: outputs discarded).
+__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false); }
+
+__device__ __forceinline__ float from_left(float v) {
+    return __builtin_bit_cast(float, dpp_from_left(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float from_right(float v) {
+    return __builtin_bit_cast(float, dpp_from_right(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double from_left(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = dpp_from_left((int)b), hi = dpp_from_left((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double from_right(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = dpp_from_right((int)b), hi = dpp_from_right((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <bool POW2, typename T>
+__device__ __forceinline__ T cdiff(T ar, T al, T two_d, T inv) {
+    if constexpr (POW2) return (ar - al) * inv;
+    else return (ar - al) / two_d;
+}
+
+// SWE tendency (weather_simulation.cpp:521-537), same evaluation order.
+template <bool POW2, typename T>
+__device__ __forceinline__ V3<T> tend(const V3<T>& c, const V3<T>& l, const V3<T>& r, const V3<T>& t,
+                                      const V3<T>& b, const Spacing<T>& sp, T g, T f) {
+    const T u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
+    const T u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
+    const T v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
+    const T v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
+    const T h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
+    const T h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
+    V3<T> k;
+    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
+    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
+    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
+    return k;
+}
+
+template <typename T>
+__device__ __forceinline__ V3<T> axpy(const V3<T>& y, T c, const V3<T>& k) {
+    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
+}
+
+// One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
+// XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
+// the neighbour index to the cell itself (weather_simulation.cpp:510-513).
+template <bool POW2, bool XCLAMP, bool YCLAMP, typename T>
+__device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
+                                            const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav,
+                                            T cor) {
+    V3<T> l{from_left(mid.u), from_left(mid.v), from_left(mid.h)};
+    V3<T> r{from_right(mid.u), from_right(mid.v), from_right(mid.h)};
+    if constexpr (XCLAMP) {
+        l = V3<T>{xlo ? mid.u : l.u, xlo ? mid.v : l.v, xlo ? mid.h : l.h};
+        r = V3<T>{xhi ? mid.u : r.u, xhi ? mid.v : r.v, xhi ? mid.h : r.h};
+    }
+    if constexpr (YCLAMP) {
+        const bool ytop = (j == 0) && g.top_clamp;
+        const bool ybot = (j == g.H - 1) && g.bot_clamp;
+        const V3<T> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
+        const V3<T> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
+        return tend<POW2>(mid, l, r, t, b, sp, grav, cor);
+    } else {
+        return tend<POW2>(mid, l, r, up, down, sp, grav, cor);
+    }
+}
+
+#ifndef WS_DPP_MINW
+#define WS_DPP_MINW 1
+#endif
+
+template <typename T, int NST, bool POW2>
+__global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
+                                                                        int nsegs) {
+    constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
+    static_assert(kYb + kPf <= kU, "y ring too short");
+
+    // XCD-aware work mapping: consecutive work items (neighbouring strips of one segment,
+    // which share halo columns) go to blocks b, b+8, ... that the dispatcher places on the
+    // same XCD (same L2). Bijective for any block count. Speed only, never correctness.
+    const int nb = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = nb / 8, rr = nb % 8, xcd = b % 8;
+    const int w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + b / 8;
+    const int strip = w % nstrips;
+    const int seg = (w / nstrips) % nsegs;
+    const int level = w / (nstrips * nsegs);
+
+    const int lane = threadIdx.x;
+    const int out_w = kWave - 2 * NST;
+    const int x = strip * out_w - NST + lane;  // this lane's global column
+    const bool xout = x >= 0 && x < g.W && lane >= NST && lane < kWave - NST;
+    const bool xlo = x == 0, xhi = x == g.W - 1;
+
+    const int y0 = seg * a.seg_rows;
+    const int y1 = min(y0 + a.seg_rows, g.H);
+    const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + NST;
+
+    const int64_t lofs = (int64_t)level * g.lstride;
+    const T* __restrict__ iu = a.in_u + lofs;
+    const T* __restrict__ iv = a.in_v + lofs;
+    const T* __restrict__ ih = a.in_h + lofs;
+    T* __restrict__ ou = a.out_u + lofs;
+    T* __restrict__ ov = a.out_v + lofs;
+    T* __restrict__ oh = a.out_h + lofs;
+
+    const int xc = min(max(x, 0), g.W - 1);
+#ifndef WS_ABLATE
+#define WS_ABLATE 0  // measurement builds only: 1 = no loads (compute only), 2 = no compute
+#endif
+    auto load_row = [&](int R) -> V3<T> {
+        const int r = min(max(R, row_lo), row_hi - 1);
+        const int64_t i = (int64_t)r * g.pitch + xc;
+        if constexpr (WS_ABLATE == 1) {
+            const T q = T(r & 7) * T(0.125) + T(xc & 3);
+            return V3<T>{q, q * T(0.5), T(10) + q};
+        } else {
+            return V3<T>{iu[i], iv[i], ih[i]};
+        }
+    };
+    auto store_row = [&](int j, const V3<T>& o) {
+        if (WS_ABLATE == 1 ? (xout && j >= y0 && j < y1 && o.u == T(12345.678)) : (xout && j >= y0 && j < y1)) {
+            const int64_t i = (int64_t)j * g.pitch + x;
+            __builtin_nontemporal_store(o.u, ou + i);
+            __builtin_nontemporal_store(o.v, ov + i);
+            __builtin_nontemporal_store(o.h, oh + i);
+        }
+    };
+
+    const V3<T> Z{T(0), T(0), T(0)};
+    V3<T> Y[kU];                 // Y[r % kU] = y row r
+    V3<T> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
+    V3<T> K2[2], K3[2];          // RK4 stage-2 / stage-3 tendencies at row r
+#pragma unroll
+    for (int i = 0; i < kU; ++i) Y[i] = Z;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) S1[i] = S2[i] = S3[i] = K2[i] = K3[i] = Z;
+
+    const int R0 = y0 - NST;
+    const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
+#pragma unroll
+    for (int i = 0; i < kPf; ++i) Y[i] = load_row(R0 + i);
+
+    auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr bool XC = decltype(Xc)::value;
+        constexpr bool YC = decltype(Yc)::value;
+        constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
+        constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
+        Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        if constexpr (WS_ABLATE == 2) {
+            store_row(R - NST, Y[yi(-NST)]);
+            return;
+        }
+        const V3<T> k1 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1,
+                                                  a.gravity, a.coriolis_f);
+        if constexpr (NST == 1) {
+            store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
+        } else {
+            const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+            const V3<T> k2 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
+                                                      a.gravity, a.coriolis_f);
+            S1[r2(-1)] = s1;
+            if constexpr (NST == 2) {
+                store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+            } else {
+                const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                const V3<T> k3 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
+                                                          a.gravity, a.coriolis_f);
+                const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
+                const V3<T> k4 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3, a.sp2,
+                                                          a.gravity, a.coriolis_f);
+                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                const T two = T(2);
+                const V3<T>& y4 = Y[yi(-4)];
+                const V3<T>& kk2 = K2[r2(-4)];
+                const V3<T>& kk3 = K3[r2(-4)];
+                V3<T> o;
+                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
+                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
+                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                store_row(R - 4, o);
+                S2[r2(-2)] = s2;
+                S3[r2(-3)] = s3;
+                K2[r2(-2)] = k2;
+                K3[r2(-3)] = k3;
+            }
+        }
+    };
+
+    auto march = [&](auto Xc, auto Yc) {
+        for (int R = R0; R < R1; R += kU) {
+            [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, R + Ps), ...);
+            }(std::make_integer_sequence<int, kU>{});
+        }
+    };
+    // global edges matter only to strips / segments within NST cells of them
+    const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - NST;
+    const bool yclamp = (g.top_clamp && y0 < NST) || (g.bot_clamp && y1 > g.H - NST);
+    if (xclamp) {
+        if (yclamp) march(std::true_type{}, std::true_type{});
+        else march(std::true_type{}, std::false_type{});
+    } else {
+        if (yclamp) march(std::false_type{}, std::true_type{});
+        else march(std::false_type{}, std::false_type{});
+    }
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
+    const int out_w = kWave - 2 * nstages;
+    const int nstrips = (g.W + out_w - 1) / out_w;
+    const int nsegs = (g.H + a.seg_rows - 1) / a.seg_rows;
+    const int64_t nblocks = (int64_t)nstrips * nsegs * g.L;
+    if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)nblocks), block(kWave);
+    const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
+#define WS_DPP_LAUNCH(N)                                                                                   \
+    if (pow2) hipLaunchKernelGGL((fused_dpp_kernel<T, N, true>), grid, block, 0, s, a, g, nstrips, nsegs);  \
+    else hipLaunchKernelGGL((fused_dpp_kernel<T, N, false>), grid, block, 0, s, a, g, nstrips, nsegs);
+    switch (nstages) {
+        case 1: WS_DPP_LAUNCH(1) break;
+        case 2: WS_DPP_LAUNCH(2) break;
+        case 4: WS_DPP_LAUNCH(4) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef WS_DPP_LAUNCH
+    return hipGetLastError();
+}
+
+template hipError_t launch_fused_step_dpp<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t);
+template hipError_t launch_fused_step_dpp<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t);
+
+}  // namespace ws

@@ -220,6 +220,7 @@ struct ws_sim {
     int64_t last_launches = 0;
     ws::KernelTimer timer;
     bool fused = true;        // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
+    bool dpp = true;          // fused kernel variant: DPP waves (WS_KERNEL=dpp) or LDS workgroups (=lds)
     int32_t seg_override = 0; // WS_SEG_ROWS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
@@ -230,9 +231,10 @@ struct ws_sim {
     int32_t seg_rows(int nst) const {
         if (seg_override > 0) return seg_override;
         const ws_grid* g = slot[0];
-        const int out_w = ws::kFusedCols - 2 * nst;
+        const int out_w = (dpp ? ws::kDppCols : ws::kFusedCols) - 2 * nst;
+        const int64_t want_blocks = dpp ? 4096 : 512;  // 64-lane vs 256-lane workgroups
         const int64_t strips = (g->W + out_w - 1) / out_w;
-        const int64_t want_segs = std::max<int64_t>(1, (512 + strips * g->L - 1) / (strips * g->L));
+        const int64_t want_segs = std::max<int64_t>(1, (want_blocks + strips * g->L - 1) / (strips * g->L));
         int64_t rows = (g->H + want_segs - 1) / want_segs;
         rows = std::max<int64_t>(rows, 24 * nst);
         rows = (rows + 2 * nst + 7) / 8 * 8 - 2 * nst;  // march length (rows + 2 NST) a multiple of the unroll
@@ -299,7 +301,8 @@ void enqueue_step(ws_sim* s) {
         a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
         a.seg_rows = s->seg_rows(nst);
         s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L, s->stream);
-        WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, s->stream));
+        WS_HIP_CHECK(s->dpp ? ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)
+                            : ws::launch_fused_step<T>(nst, a, g, s->stream));
         s->timer.end(s->stream);
         ++s->last_launches;
     } else if (method == WS_EULER) {
@@ -404,6 +407,7 @@ ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
+        if (const char* e = std::getenv("WS_KERNEL")) s->dpp = std::strcmp(e, "lds") != 0;
         if (const char* e = std::getenv("WS_SEG_ROWS")) s->seg_override = std::atoi(e);
         const int method = effective_method(*cfg);
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);

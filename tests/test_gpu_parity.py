@@ -56,10 +56,15 @@ def load(sim, s0):
     g.set_humidity_field(s0["q"])
 
 
-@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused_step_kernel", "stage_kernels"])
+KERNELS = [("1", "dpp"), ("1", "lds"), ("0", "dpp")]
+KERNEL_IDS = ["fused_dpp", "fused_lds", "stage_kernels"]
+
+
+@pytest.mark.parametrize("fused,kernel", KERNELS, ids=KERNEL_IDS)
 @pytest.mark.parametrize("variant", ["f32", "f64"])
-def test_stepping_bitwise(variant, fused, monkeypatch):
+def test_stepping_bitwise(variant, fused, kernel, monkeypatch):
     monkeypatch.setenv("WS_FUSED", fused)
+    monkeypatch.setenv("WS_KERNEL", kernel)
     gold = golden(variant)
     cases = gold.cases("step/")
     assert len(cases) >= 20
@@ -267,15 +272,17 @@ def test_pe_levels_match_reference_per_level():
             assert _digest(got[f]) == h, (k, f)
 
 
+@pytest.mark.parametrize("kernel", ["dpp", "lds"])
 @pytest.mark.parametrize("seg_rows", ["0", "5", "33"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_fused_tiling_vs_oracle(fp64, method, seg_rows, monkeypatch):
+def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, monkeypatch):
     """Strip (x) and segment (y) seams of the fused kernel: 700 x 77 grid spans three
     256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle."""
     from oracle.ws_oracle import OracleSim
 
     monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
+    monkeypatch.setenv("WS_KERNEL", kernel)
     W, H = 700, 77
     sim = make_sim(W, H, 0, method, fp64, dx=1.0, dy=2.0, f=0.3)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
