@@ -52,6 +52,33 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _new_uid(native):
+    import ctypes
+    buf = (ctypes.c_uint8 * native.COMM_ID_BYTES)()
+    native.check(native.lib.ws_comm_get_unique_id(buf))
+    return bytes(buf)
+
+
+def bootstrap_uid(dist, rank, make_uid, nbytes=128):
+    """Rank 0 creates the RCCL unique id; every rank receives it over the (gloo) host group."""
+    import torch
+    uid = torch.zeros(nbytes, dtype=torch.uint8)
+    if rank == 0:
+        raw = make_uid()
+        assert len(raw) == nbytes
+        uid = torch.tensor(list(raw), dtype=torch.uint8)
+    dist.broadcast(uid, 0)
+    return bytes(uid.tolist())
+
+
+def max_over_ranks(dist, seconds):
+    """The contract's job time: the slowest rank's."""
+    import torch
+    t = torch.tensor([seconds], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
 def cpu_baseline(conf, method, budget_s=20.0):
     """Time the reference CPU solver (or the oracle port) on a bounded sample."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -137,14 +164,8 @@ def main():
     cfg.max_time = 1e30  # run() would otherwise stop at t >= 10 (1000 steps of dt = 0.01)
 
     if world > 1:
-        import ctypes
-        uid = torch.zeros(_native.COMM_ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            buf = (ctypes.c_uint8 * _native.COMM_ID_BYTES)()
-            _native.check(_native.lib.ws_comm_get_unique_id(buf))
-            uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
-        dist.broadcast(uid, 0)
-        sim = ws.WeatherSimulation(cfg, _slab=(rank, world, bytes(uid.tolist())))
+        uid = bootstrap_uid(dist, rank, lambda: _new_uid(_native))
+        sim = ws.WeatherSimulation(cfg, _slab=(rank, world, uid))
     else:
         sim = ws.WeatherSimulation(cfg)
 
@@ -168,9 +189,7 @@ def main():
     elapsed = time.perf_counter() - t0
     assert taken == args.steps, (taken, args.steps)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
+        elapsed = max_over_ranks(dist, elapsed)
 
     cells = conf["W"] * conf["H"] * conf["L"]
     value = cells * args.steps / elapsed

@@ -214,6 +214,16 @@ int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]);
 int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
                        ws_sim_t** out, int32_t* row0, int32_t* rows);
 
+/* Slab group: the same y-slab decomposition and step schedule (interior segments while the
+ * halo moves, then edge segments) inside ONE process on one device, halo rows moved by
+ * device copies. Used to verify the decomposition bitwise against the single-domain run
+ * on a single GPU. Slabs are owned by the group and step only through ws_group_run. */
+typedef struct ws_group ws_group_t;
+int ws_group_create(const ws_config_t* cfg, int32_t nslabs, ws_group_t** out);
+int ws_group_destroy(ws_group_t* group);
+int ws_group_slab(ws_group_t* group, int32_t rank, ws_sim_t** sim, int32_t* row0, int32_t* rows);
+int ws_group_run(ws_group_t* group, int32_t num_steps, int32_t* steps_taken);
+
 /* Row range [row0, row0 + rows) of rank `rank` in the balanced split of `height` rows. */
 int ws_slab_partition(int32_t height, int32_t rank, int32_t nranks, int32_t* row0, int32_t* rows);
 /* Collectives on the slab communicator (max over ranks of one double; barrier). On a

@@ -18,7 +18,14 @@ struct FusedArgs {
     Spacing<T> sp1;               // stage 1: spacing of the current grid
     Spacing<T> sp2;               // later stages: spacing of the temp grid (= config)
     int32_t seg_rows;             // output rows per workgroup segment
+    // segments processed by this launch: local index i < seg_na -> seg_a + i,
+    // else seg_b + (i - seg_na); seg_n in total (slab interior / edge split)
+    int32_t seg_a, seg_na, seg_b, seg_n;
 };
+
+__host__ __device__ inline int fused_segment(int i, int seg_a, int seg_na, int seg_b) {
+    return i < seg_na ? seg_a + i : seg_b + (i - seg_na);
+}
 
 // nstages: 1 (Euler), 2 (RK2 midpoint), 4 (RK4-as-implemented)
 // LDS variant: 256-lane workgroups, horizontal neighbours through LDS, one barrier per row.

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
     T* const clampcol = lds.col(x == 0 ? lane : (x == g.W - 1 ? lane + 2 : (xlive ? lane + 1 : 0)));
     const T* const lcol = lds.col(lane);  // left neighbour column; right = lcol + 2 kCs
 
-    const int y0 = blockIdx.y * a.seg_rows;
+    const int y0 = fused_segment(blockIdx.y, a.seg_a, a.seg_na, a.seg_b) * a.seg_rows;
     const int y1 = min(y0 + a.seg_rows, g.H);
     const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
     const int row_hi = g.bot_clamp ? g.H : g.H + NST;
@@ -269,7 +269,8 @@ template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
     if (g.W < 2) return hipErrorInvalidValue;  // x = 0 == W-1 needs two clamp copies: use the stage kernels
     const int out_w = kFusedCols - 2 * nstages;
-    const dim3 grid((g.W + out_w - 1) / out_w, (g.H + a.seg_rows - 1) / a.seg_rows, g.L);
+    if (a.seg_n <= 0) return hipSuccess;
+    const dim3 grid((g.W + out_w - 1) / out_w, a.seg_n, g.L);
     const dim3 block(kFusedCols);
     const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
 #define WS_FUSED_LAUNCH(N)                                                                               \

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const int q = nb / 8, rr = nb % 8, xcd = b % 8;
     const int w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + b / 8;
     const int strip = w % nstrips;
-    const int seg = (w / nstrips) % nsegs;
+    const int seg = fused_segment((w / nstrips) % nsegs, a.seg_a, a.seg_na, a.seg_b);
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
@@ -250,7 +250,8 @@ template <typename T>
 hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
     const int out_w = kWave - 2 * nstages;
     const int nstrips = (g.W + out_w - 1) / out_w;
-    const int nsegs = (g.H + a.seg_rows - 1) / a.seg_rows;
+    const int nsegs = a.seg_n;
+    if (nsegs <= 0) return hipSuccess;
     const int64_t nblocks = (int64_t)nstrips * nsegs * g.L;
     if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblocks), block(kWave);

@@ -219,7 +219,12 @@ struct ws_sim {
     double last_ms = 0.0;
     int64_t last_launches = 0;
     ws::KernelTimer timer;
-    bool fused = true;        // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
+    int32_t rank = 0, nranks = 1;                       // y-slab position (1 = whole domain)
+    hipStream_t comm_stream = nullptr;                  // RCCL halo exchange (overlaps interior segments)
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    bool own_stream = true;
+    bool in_group = false;                              // a slab of a ws_group (local halo transport)
+    bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
     bool dpp = true;          // fused kernel variant: DPP waves (WS_KERNEL=dpp) or LDS workgroups (=lds)
     int32_t seg_override = 0; // WS_SEG_ROWS
     // slab decomposition
@@ -276,36 +281,90 @@ void launch(ws_sim* s, int mode, const ws::StageArgs<T>& a, const ws_grid* in, i
     ++s->last_launches;
 }
 
-// One time step on the stream (no host synchronisation).
+int fused_stages(const ws_sim* s) {
+    const int m = effective_method(s->cfg);
+    return m == WS_EULER ? 1 : m == WS_RK2 ? 2 : 4;
+}
+
+bool use_fused(const ws_sim* s) { return s->fused && s->slot[0]->W >= 2; }
+
+// Segments of a slab whose dependency cone (rows [y0 - nst, y1 + nst)) stays inside the
+// owned rows need no halo: they run while the halo exchange is in flight ("interior",
+// segments [k0, k1)); the others run after it ("edge").
+struct SegSplit {
+    int nsegs, k0, k1;
+};
+
+SegSplit seg_split(const ws_sim* s, int nst) {
+    const ws_grid* g = s->slot[0];
+    const int seg = s->seg_rows(nst);
+    SegSplit p;
+    p.nsegs = (g->H + seg - 1) / seg;
+    p.k0 = g->top_clamp ? 0 : (nst + seg - 1) / seg;
+    p.k1 = g->bot_clamp ? p.nsegs : std::max(0, (g->H - nst) / seg);
+    p.k0 = std::min(p.k0, p.nsegs);
+    p.k1 = std::max(p.k1, p.k0);
+    return p;
+}
+
+// Launch the fused step kernel over segments [segA, segA + nA) U [segB, segB + nB).
 template <typename T>
-void enqueue_step(ws_sim* s) {
+void fused_launch(ws_sim* s, int nst, int segA, int nA, int segB, int nB) {
+    if (nA + nB <= 0) return;
     ws_grid* c = s->slot[s->cur];
     ws_grid* n = s->slot[1 - s->cur];
     const T dt = (T)s->dt;
-    const T half = T(0.5f) * dt;  // `0.5f * dt_` (weather_simulation.cpp:249)
+    ws::FusedArgs<T> a{};
+    a.in_u = (const T*)c->f[0]; a.in_v = (const T*)c->f[1]; a.in_h = (const T*)c->f[2];
+    a.out_u = (T*)n->f[0]; a.out_v = (T*)n->f[1]; a.out_h = (T*)n->f[2];
+    a.c_half = T(0.5f) * dt;  // `0.5f * dt_` (weather_simulation.cpp:249)
+    a.c_dt = dt;
+    a.c_dt6 = dt / T(6.0f);   // `dt_ / 6.0f` (:438)
+    a.gravity = (T)s->cfg.gravity;
+    a.coriolis_f = (T)s->cfg.coriolis_f;
+    a.sp1 = make_spacing<T>(c->dx, c->dy);
+    a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
+    a.seg_rows = s->seg_rows(nst);
+    a.seg_a = segA;
+    a.seg_na = nA;
+    a.seg_b = segB;
+    a.seg_n = nA + nB;
+    const ws::Geom g = c->geom();
+    WS_HIP_CHECK(s->dpp ? ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)
+                        : ws::launch_fused_step<T>(nst, a, g, s->stream));
+    ++s->last_launches;
+}
+
+// Phase 1 of a step: everything that does not need this step's halo rows.
+//  * single domain: the whole step (fused or stage kernels);
+//  * slab, fused: start the RCCL halo exchange on the comm stream (after the previous
+//    step's output is complete) and run the interior segments meanwhile.
+template <typename T>
+void step_begin(ws_sim* s) {
+    ws_grid* c = s->slot[s->cur];
+    ws_grid* n = s->slot[1 - s->cur];
+    const T dt = (T)s->dt;
+    const T half = T(0.5f) * dt;
     const int method = effective_method(s->cfg);
-    if (s->fused && c->W >= 2) {
-        // one kernel per step: all stages on chip, y read once, y' written once (6 words/cell)
-        const int nst = method == WS_EULER ? 1 : method == WS_RK2 ? 2 : 4;
-        const ws::Geom g = c->geom();
-        if (s->comm) s->comm->exchange(c->f, 3, (int)sizeof(T), g, nst, s->stream);
-        ws::FusedArgs<T> a{};
-        a.in_u = (const T*)c->f[0]; a.in_v = (const T*)c->f[1]; a.in_h = (const T*)c->f[2];
-        a.out_u = (T*)n->f[0]; a.out_v = (T*)n->f[1]; a.out_h = (T*)n->f[2];
-        a.c_half = half;
-        a.c_dt = dt;
-        a.c_dt6 = dt / T(6.0f);
-        a.gravity = (T)s->cfg.gravity;
-        a.coriolis_f = (T)s->cfg.coriolis_f;
-        a.sp1 = make_spacing<T>(c->dx, c->dy);
-        a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
-        a.seg_rows = s->seg_rows(nst);
+    const ws::Geom g = c->geom();
+    if (use_fused(s)) {
+        const int nst = fused_stages(s);
+        const SegSplit p = seg_split(s, nst);
         s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L, s->stream);
-        WS_HIP_CHECK(s->dpp ? ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)
-                            : ws::launch_fused_step<T>(nst, a, g, s->stream));
-        s->timer.end(s->stream);
-        ++s->last_launches;
-    } else if (method == WS_EULER) {
+        if (s->nranks == 1) {
+            fused_launch<T>(s, nst, 0, p.nsegs, 0, 0);
+            return;
+        }
+        if (s->comm) {
+            WS_HIP_CHECK(hipEventRecord(s->ev_ready, s->stream));
+            WS_HIP_CHECK(hipStreamWaitEvent(s->comm_stream, s->ev_ready, 0));
+            s->comm->exchange(c->f, 3, (int)sizeof(T), g, nst, s->comm_stream);
+            WS_HIP_CHECK(hipEventRecord(s->ev_halo, s->comm_stream));
+        }
+        fused_launch<T>(s, nst, p.k0, p.k1 - p.k0, 0, 0);
+        return;
+    }
+    if (method == WS_EULER) {
         launch<T>(s, ws::kAxpy, stage_args<T>(c, c, n, dt, s), c, 0, 6);
     } else if (method == WS_RK2) {
         launch<T>(s, ws::kAxpy, stage_args<T>(c, c, s->tmpA, half, s), c, 0, 6);
@@ -323,6 +382,24 @@ void enqueue_step(ws_sim* s) {
         a4.k3_u = (const T*)s->K3->f[0]; a4.k3_v = (const T*)s->K3->f[1]; a4.k3_h = (const T*)s->K3->f[2];
         launch<T>(s, ws::kRk4Final, a4, s->tmpA, 3, 15);
     }
+}
+
+// Phase 2: the segments that need the halo (after it arrived), the PE T/P update, and the
+// grid rotation of the reference (current <-> next shared_ptr swap).
+template <typename T>
+void step_end(ws_sim* s) {
+    ws_grid* c = s->slot[s->cur];
+    ws_grid* n = s->slot[1 - s->cur];
+    const T dt = (T)s->dt;
+    if (use_fused(s)) {
+        if (s->nranks > 1) {
+            const int nst = fused_stages(s);
+            const SegSplit p = seg_split(s, nst);
+            if (s->comm) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_halo, 0));
+            fused_launch<T>(s, nst, 0, p.k0, p.k1, p.nsegs - p.k1);
+        }
+        s->timer.end(s->stream);
+    }
     if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
         // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
         const ws::Geom g = c->geom();
@@ -332,6 +409,13 @@ void enqueue_step(ws_sim* s) {
     }
     s->cur = 1 - s->cur;
     s->slot[s->cur]->diag_pending = true;  // step() ends with calculateDiagnostics (:149)
+}
+
+// One time step on the stream (no host synchronisation).
+template <typename T>
+void enqueue_step(ws_sim* s) {
+    step_begin<T>(s);
+    step_end<T>(s);
 }
 
 template <typename T>
@@ -357,6 +441,7 @@ int plan_steps(const ws_sim* s, int n) {
 }
 
 void run_steps(ws_sim* s, int k) {
+    require(!s->in_group, WS_ERR_INVALID, "a slab of a group steps only with ws_group_run");
     set_device(s->device);
     s->last_launches = 0;
     WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
@@ -367,6 +452,14 @@ void run_steps(ws_sim* s, int k) {
         s->step++;
     }
     WS_HIP_CHECK(hipEventRecord(s->ev1, s->stream));
+    if (k > 0 && s->comm) {
+        // Diagnostics at slab seams read the neighbours' CURRENT rows: every rank refreshes a
+        // one-row u, v halo and computes them here, collectively (a lazy per-rank exchange
+        // would deadlock when only one rank reads vorticity).
+        ws_grid* c = s->slot[s->cur];
+        s->comm->exchange(c->f, 2, (int)elem_size(s->dtype), c->geom(), 1, s->stream);
+        materialize_diag(c);
+    }
     WS_HIP_CHECK(hipEventSynchronize(s->ev1));
     s->timer.collect();
     float ms = 0.f;
@@ -380,14 +473,24 @@ void run_steps(ws_sim* s, int k) {
 void sim_free(ws_sim* s) {
     for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
         if (g) { grid_free(g); delete g; }
-    if (s->ev0) (void)hipEventDestroy(s->ev0);
-    if (s->ev1) (void)hipEventDestroy(s->ev1);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    for (hipEvent_t e : {s->ev0, s->ev1, s->ev_ready, s->ev_halo})
+        if (e) (void)hipEventDestroy(e);
+    if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
+    if (s->comm_stream) (void)hipStreamDestroy(s->comm_stream);
     delete s->comm;
     delete s;
 }
 
-ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm, int32_t row0) {
+// Where a simulation sits in a y-slab decomposition (rank 0 of 1: the whole domain).
+struct SlabInfo {
+    int32_t rank = 0, nranks = 1, row0 = 0, rows = 0;
+};
+
+// cfg describes the GLOBAL grid; the simulation owns rows [row0, row0 + rows). `stream`:
+// use this (caller-owned) stream instead of creating one (slabs of a group share one).
+ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hipStream_t stream = nullptr) {
+    const int32_t local_rows = slab.nranks == 1 ? (cfg ? cfg->grid_height : 0) : slab.rows;
+    const int32_t row0 = slab.row0;
     require(cfg != nullptr, WS_ERR_INVALID, "null config");
     require(cfg->grid_width > 0 && cfg->grid_height > 0 && cfg->num_levels > 0, WS_ERR_INVALID,
             "Grid dimensions must be positive");
@@ -400,10 +503,26 @@ ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm
     s->dt = to_prec(cfg->dt, s->dtype);
     s->comm = comm;
     s->row0 = row0;
+    s->rank = slab.rank;
+    s->nranks = slab.nranks;
     try {
-        WS_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        if (stream) {
+            s->stream = stream;
+            s->own_stream = false;
+        } else {
+            WS_HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        }
         WS_HIP_CHECK(hipEventCreate(&s->ev0));
         WS_HIP_CHECK(hipEventCreate(&s->ev1));
+        if (comm) {
+            // highest priority: the exchange's few workgroups must not queue behind the
+            // interior segments' thousands
+            int lo = 0, hi = 0;
+            WS_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            WS_HIP_CHECK(hipStreamCreateWithPriority(&s->comm_stream, hipStreamNonBlocking, hi));
+            WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
+            WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
+        }
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
@@ -421,9 +540,9 @@ ws_sim* sim_build(const ws_config_t* cfg, int32_t local_rows, ws::SlabComm* comm
             g->owned = true;
             g->dx = to_prec(cfg->dx, s->dtype);
             g->dy = to_prec(cfg->dy, s->dtype);
-            if (comm) {
-                g->top_clamp = comm->rank() == 0;
-                g->bot_clamp = comm->rank() == comm->nranks() - 1;
+            if (slab.nranks > 1) {
+                g->top_clamp = slab.rank == 0;
+                g->bot_clamp = slab.rank == slab.nranks - 1;
                 g->row0 = row0;
                 g->gH = cfg->grid_height;
             }
@@ -681,13 +800,14 @@ int ws_grid_apply_initial_condition(ws_grid_t* g, const char* name, const double
 int ws_sim_create(const ws_config_t* cfg, ws_sim_t** out) {
     return guarded([&] {
         require(out != nullptr, WS_ERR_INVALID, "null pointer");
-        *out = sim_build(cfg, cfg ? cfg->grid_height : 0, nullptr, 0);
+        *out = sim_build(cfg, SlabInfo{}, nullptr);
     });
 }
 
 int ws_sim_destroy(ws_sim_t* s) {
     return guarded([&] {
         if (!s) return;
+        require(!s->in_group, WS_ERR_INVALID, "simulation is owned by a slab group");
         set_device(s->device);
         (void)hipStreamSynchronize(s->stream);
         sim_free(s);
@@ -951,12 +1071,17 @@ int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, con
         require(cfg->grid_height >= nranks, WS_ERR_INVALID, "fewer rows than ranks");
         int r0 = 0, nrows = 0;
         ws::slab_rows(cfg->grid_height, rank, nranks, &r0, &nrows);
+        require(nranks == 1 || nrows >= ws::kHalo, WS_ERR_INVALID, "a slab needs at least 4 rows per rank");
         const int r1 = r0 + nrows;
         set_device(cfg->device_id);
+        // a 1-rank slab still gets its communicator: same code path as N>1 (the exchanges
+        // are no-ops), so a 1-GPU run exercises the RCCL bootstrap
         ws::SlabComm* comm = new ws::SlabComm(rank, nranks, id);
         ws_sim* s = nullptr;
         try {
-            s = sim_build(cfg, r1 - r0, comm, r0);
+            SlabInfo si;
+            si.rank = rank; si.nranks = nranks; si.row0 = r0; si.rows = nrows;
+            s = sim_build(cfg, si, comm, nullptr);
         } catch (...) {
             delete comm;
             throw;
@@ -1011,6 +1136,145 @@ int ws_sim_comm_barrier(ws_sim_t* s) {
         set_device(s->device);
         if (s->comm) s->comm->barrier(s->stream);
         WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+    });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------
+// slab group: the y-slab decomposition inside one process on one device, halo rows moved
+// by device copies instead of RCCL. It runs exactly the multi-rank step schedule
+// (interior segments -> halo exchange -> edge segments) and is how the decomposition is
+// verified bitwise against the single-domain run on a one-GPU box.
+// ------------------------------------------------------------------------------------
+struct ws_group {
+    std::vector<ws_sim*> slabs;
+    hipStream_t stream = nullptr;
+    int device = 0;
+};
+
+namespace {
+
+// pull `depth` halo rows of u, v, h for slab r from its neighbours' current grids
+template <typename T>
+void group_exchange(ws_group* gr, int r, int depth) {
+    ws_sim* s = gr->slabs[r];
+    const ws_grid* me = s->slot[s->cur];
+    const size_t es = sizeof(T), row = (size_t)me->pitch * es, bytes = row * depth;
+    for (int f = 0; f < 3; ++f) {
+        for (int l = 0; l < me->L; ++l) {
+            char* mine = (char*)me->f[f] + (size_t)l * me->lstride * es;
+            if (r > 0) {
+                const ws_grid* up = gr->slabs[r - 1]->slot[gr->slabs[r - 1]->cur];
+                const char* src = (const char*)up->f[f] + (size_t)l * up->lstride * es + (size_t)(up->H - depth) * row;
+                WS_HIP_CHECK(hipMemcpyAsync(mine - bytes, src, bytes, hipMemcpyDeviceToDevice, gr->stream));
+            }
+            if (r + 1 < (int)gr->slabs.size()) {
+                const ws_grid* dn = gr->slabs[r + 1]->slot[gr->slabs[r + 1]->cur];
+                const char* src = (const char*)dn->f[f] + (size_t)l * dn->lstride * es;
+                WS_HIP_CHECK(hipMemcpyAsync(mine + (size_t)me->H * row, src, bytes, hipMemcpyDeviceToDevice,
+                                            gr->stream));
+            }
+        }
+    }
+}
+
+template <typename T>
+void group_step(ws_group* gr) {
+    for (ws_sim* s : gr->slabs) step_begin<T>(s);
+    const int depth = fused_stages(gr->slabs[0]);
+    for (int r = 0; r < (int)gr->slabs.size(); ++r) group_exchange<T>(gr, r, depth);
+    for (ws_sim* s : gr->slabs) step_end<T>(s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ws_group_create(const ws_config_t* cfg, int32_t nslabs, ws_group_t** out) {
+    return guarded([&] {
+        require(cfg && out, WS_ERR_INVALID, "null pointer");
+        require(nslabs >= 1 && cfg->grid_height >= nslabs * ws::kHalo, WS_ERR_INVALID, "a slab needs >= 4 rows");
+        set_device(cfg->device_id);
+        ws_group* gr = new ws_group;
+        gr->device = cfg->device_id;
+        try {
+            WS_HIP_CHECK(hipStreamCreateWithFlags(&gr->stream, hipStreamNonBlocking));
+            for (int r = 0; r < nslabs; ++r) {
+                SlabInfo si;
+                si.rank = r;
+                si.nranks = nslabs;
+                ws::slab_rows(cfg->grid_height, r, nslabs, &si.row0, &si.rows);
+                ws_sim* s = sim_build(cfg, si, nullptr, gr->stream);
+                s->in_group = true;
+                gr->slabs.push_back(s);
+                require(use_fused(s), WS_ERR_UNSUPPORTED, "slab groups need the fused step kernel (WS_FUSED=1)");
+            }
+        } catch (...) {
+            for (ws_sim* s : gr->slabs) sim_free(s);
+            if (gr->stream) (void)hipStreamDestroy(gr->stream);
+            delete gr;
+            throw;
+        }
+        *out = gr;
+    });
+}
+
+int ws_group_destroy(ws_group_t* gr) {
+    return guarded([&] {
+        if (!gr) return;
+        set_device(gr->device);
+        (void)hipStreamSynchronize(gr->stream);
+        for (ws_sim* s : gr->slabs) sim_free(s);
+        (void)hipStreamDestroy(gr->stream);
+        delete gr;
+    });
+}
+
+int ws_group_slab(ws_group_t* gr, int32_t rank, ws_sim_t** sim, int32_t* row0, int32_t* rows) {
+    return guarded([&] {
+        require(gr && sim && rank >= 0 && rank < (int)gr->slabs.size(), WS_ERR_INVALID, "bad argument");
+        ws_sim* s = gr->slabs[rank];
+        *sim = s;
+        if (row0) *row0 = s->row0;
+        if (rows) *rows = s->slot[0]->H;
+    });
+}
+
+int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
+    return guarded([&] {
+        require(gr != nullptr, WS_ERR_INVALID, "null group");
+        set_device(gr->device);
+        const int k = plan_steps(gr->slabs[0], n);
+        ws_sim* s0 = gr->slabs[0];
+        WS_HIP_CHECK(hipEventRecord(s0->ev0, gr->stream));
+        for (int i = 0; i < k; ++i) {
+            if (s0->dtype == WS_F64) group_step<double>(gr);
+            else group_step<float>(gr);
+            for (ws_sim* s : gr->slabs) {
+                s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
+                s->step++;
+            }
+        }
+        WS_HIP_CHECK(hipEventRecord(s0->ev1, gr->stream));
+        if (k > 0) {  // seam diagnostics need the neighbours' current rows (see run_steps)
+            for (int r = 0; r < (int)gr->slabs.size(); ++r)
+                if (s0->dtype == WS_F64) group_exchange<double>(gr, r, 1);
+                else group_exchange<float>(gr, r, 1);
+            for (ws_sim* s : gr->slabs) materialize_diag(s->slot[s->cur]);
+        }
+        WS_HIP_CHECK(hipStreamSynchronize(gr->stream));
+        WS_HIP_CHECK(hipEventSynchronize(s0->ev1));
+        float ms = 0.f;
+        WS_HIP_CHECK(hipEventElapsedTime(&ms, s0->ev0, s0->ev1));
+        for (ws_sim* s : gr->slabs) {
+            s->timer.collect();
+            s->last_ms = ms;
+            s->metrics.compute_time_ms += ms;
+            s->metrics.total_time_ms += ms;
+            s->metrics.num_steps += k;
+        }
+        if (taken) *taken = k;
     });
 }
 

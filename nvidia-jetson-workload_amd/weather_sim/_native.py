@@ -108,6 +108,10 @@ SIGNATURES = {
     "ws_slab_partition": [_I, _I, _I, _PI, _PI],
     "ws_sim_comm_allreduce_max": [_P, _D, _PD],
     "ws_sim_comm_barrier": [_P],
+    "ws_group_create": [ctypes.POINTER(ws_config_t), _I, _PP],
+    "ws_group_destroy": [_P],
+    "ws_group_slab": [_P, _I, _PP, _PI, _PI],
+    "ws_group_run": [_P, _I, _PI],
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
 }

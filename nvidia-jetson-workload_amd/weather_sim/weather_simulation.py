@@ -515,8 +515,17 @@ _BACKEND_NAMES = {0: "HIP GPU (MI355X)", 1: "HIP GPU (MI355X; CPU requested)", 2
 
 
 class WeatherSimulation:
-    def __init__(self, config: SimulationConfig, _slab=None):
+    def __init__(self, config: SimulationConfig, _slab=None, _handle=None, _owner=None):
         self._config_py = config
+        self._owner = _owner
+        self._ic = None
+        self._om = None
+        if _handle is not None:  # a slab owned by a SlabGroup
+            self._h = ctypes.c_void_p(_handle)
+            self._owned = False
+            self.row0, self.rows = _slab
+            return
+        self._owned = True
         c = config._to_c()
         h = ctypes.c_void_p()
         self.row0, self.rows = 0, config.grid_height
@@ -530,12 +539,10 @@ class WeatherSimulation:
                                          ctypes.byref(r0), ctypes.byref(nr)))
             self.row0, self.rows = r0.value, nr.value
         self._h = h
-        self._ic = None
-        self._om = None
         _say(f"Using compute backend: {_BACKEND_NAMES.get(int(config.compute_backend), 'HIP GPU (MI355X)')}")
 
     def __del__(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_owned", False) and getattr(self, "_h", None):
             lib.ws_sim_destroy(self._h)
             self._h = None
 
@@ -667,6 +674,60 @@ class WeatherSimulation:
 
     def comm_barrier(self):
         check(lib.ws_sim_comm_barrier(self._h))
+
+
+class SlabGroup:
+    """Extension: the y-slab decomposition of one global grid inside one process on one
+    device (halo rows by device copies, same step schedule as the multi-GPU RCCL path).
+    `slab(r)` is a WeatherSimulation view of rank r's rows [row0, row0 + rows)."""
+
+    def __init__(self, config: SimulationConfig, nslabs: int):
+        self._config_py = config
+        c = config._to_c()
+        h = ctypes.c_void_p()
+        check(lib.ws_group_create(ctypes.byref(c), int(nslabs), ctypes.byref(h)))
+        self._h = h
+        self.nslabs = int(nslabs)
+        self._slabs = []
+        for r in range(self.nslabs):
+            s, r0, nr = ctypes.c_void_p(), ctypes.c_int32(), ctypes.c_int32()
+            check(lib.ws_group_slab(self._h, r, ctypes.byref(s), ctypes.byref(r0), ctypes.byref(nr)))
+            self._slabs.append(WeatherSimulation(config, _slab=(r0.value, nr.value), _handle=s.value, _owner=self))
+        self._ic = None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._slabs = []
+            lib.ws_group_destroy(self._h)
+            self._h = None
+
+    def slab(self, rank):
+        return self._slabs[rank]
+
+    def set_initial_condition(self, ic):
+        self._ic = ic
+
+    def initialize(self):
+        for s in self._slabs:
+            check(lib.ws_sim_initialize(s._h))
+            if self._ic is not None:
+                self._ic.initialize(s.get_current_grid())  # global coordinates, own rows
+
+    def run(self, num_steps):
+        taken = ctypes.c_int32()
+        check(lib.ws_group_run(self._h, int(num_steps), ctypes.byref(taken)))
+        return taken.value
+
+    def gather(self, name):
+        """The global (H, W) (or (L, H, W)) field assembled from the slabs."""
+        parts = [s.get_current_grid()._get(name) for s in self._slabs]
+        return np.concatenate(parts, axis=-2)
+
+    def scatter(self, name, arr):
+        """Set a global field from a (H, W) / (L, H, W) array."""
+        a = np.asarray(arr)
+        for s in self._slabs:
+            s.get_current_grid()._set(name, a[..., s.row0:s.row0 + s.rows, :])
 
 
 # ---------------------------------------------------------------------------------

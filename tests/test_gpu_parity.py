@@ -320,3 +320,60 @@ def test_fused_non_pow2_spacing_vs_oracle():
     got = state(sim.get_current_grid())
     for k in ("u", "v", "h", "vort"):
         np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
+
+
+@pytest.mark.parametrize("kernel,seg_rows", [("dpp", "0"), ("dpp", "6"), ("lds", "6")])
+@pytest.mark.parametrize("nslabs", [2, 3, 5])
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_slab_group_matches_single_domain(fp64, method, nslabs, kernel, seg_rows, monkeypatch):
+    """y-slab decomposition (interior segments, halo exchange, edge segments) == one domain,
+    bit-for-bit, for uneven slab heights and several segment sizes."""
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
+    W, H, steps = 300, 83, 7
+
+    def cfg():
+        c = ws.SimulationConfig()
+        c.grid_width, c.grid_height = W, H
+        c.integration_method, c.double_precision = method, fp64
+        c.dx, c.dy, c.coriolis_f = 1.0, 2.0, 0.25
+        return c
+
+    ic = ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0)
+    one = ws.WeatherSimulation(cfg())
+    one.set_initial_condition(ic)
+    one.initialize()
+    group = ws.SlabGroup(cfg(), nslabs)
+    group.set_initial_condition(ic)
+    group.initialize()
+    for name in ("u", "v", "h"):  # the IC evaluated per slab in global coordinates
+        np.testing.assert_array_equal(group.gather(name), one.get_current_grid()._get(name), err_msg=f"ic {name}")
+    assert group.run(steps) == steps
+    one.run(steps)
+    g1 = one.get_current_grid()
+    for name in ("u", "v", "h", "vorticity", "divergence"):
+        np.testing.assert_array_equal(group.gather(name), g1._get(name), err_msg=name)
+    assert group.slab(nslabs - 1).get_current_time() == one.get_current_time()
+
+
+def test_slab_group_levels_and_pe():
+    """PE (T/P drift) with 3 levels over 4 slabs == one domain."""
+    W, H, L = 130, 40, 3
+
+    def cfg():
+        c = ws.SimulationConfig()
+        c.grid_width, c.grid_height, c.num_levels = W, H, L
+        c.model, c.integration_method = ws.SimulationModel.PrimitiveEquations, ws.IntegrationMethod.RungeKutta4
+        return c
+
+    one = ws.WeatherSimulation(cfg())
+    one.set_initial_condition(ws.FrontInitialCondition())
+    one.initialize()
+    group = ws.SlabGroup(cfg(), 4)
+    group.set_initial_condition(ws.FrontInitialCondition())
+    group.initialize()
+    group.run(5)
+    one.run(5)
+    for name in ("u", "v", "h", "t", "p", "q"):
+        np.testing.assert_array_equal(group.gather(name), one.get_current_grid()._get(name), err_msg=name)
