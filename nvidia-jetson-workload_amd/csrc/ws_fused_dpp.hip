@@ -28,9 +28,11 @@ struct V3 {
 };
 
 // lane i <- lane i-1 (value of the left column) / lane i <- lane i+1 (right column).
-// Lanes without a source keep their own value (edge lanes of a strip: outputs discarded).
-__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false); }
-__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false); }
+// Lanes without a source read 0 (bound_ctrl): they are a strip's edge lanes, whose results
+// lie in the discarded NST-lane margin. (Keeping the lane's own value instead would cost a
+// v_mov per DPP to pre-load the destination: 48 VALU per row in fp64 RK4.)
+__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true); }
 
 __device__ __forceinline__ float from_left(float v) {
     return __builtin_bit_cast(float, dpp_from_left(__builtin_bit_cast(int, v)));
@@ -47,6 +49,27 @@ __device__ __forceinline__ double from_right(double v) {
     const long long b = __builtin_bit_cast(long long, v);
     const int lo = dpp_from_right((int)b), hi = dpp_from_right((int)(b >> 32));
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+template <typename T>
+__device__ __forceinline__ void buf_store_nt(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    constexpr int kNT = 2;  // cache policy: nontemporal (streaming output, never re-read this step)
+    if constexpr (sizeof(T) == 8) {
+        using U2 = unsigned int __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, kNT);
+    }
 }
 
 template <bool POW2, typename T>
@@ -133,34 +156,46 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
     const int row_hi = g.bot_clamp ? g.H : g.H + NST;
 
+    // Buffer addressing: one descriptor per field, based at this wave's first row (all
+    // wave-uniform, SGPRs), the row as a scalar byte offset, the lane's column as a fixed
+    // 32-bit voffset -- no per-row VALU address arithmetic. Stores of lanes outside the
+    // strip's output columns get an out-of-range voffset: the buffer range check drops them
+    // (no exec-mask branch). launch_fused_step_dpp checks the byte ranges fit.
     const int64_t lofs = (int64_t)level * g.lstride;
-    const T* __restrict__ iu = a.in_u + lofs;
-    const T* __restrict__ iv = a.in_v + lofs;
-    const T* __restrict__ ih = a.in_h + lofs;
-    T* __restrict__ ou = a.out_u + lofs;
-    T* __restrict__ ov = a.out_v + lofs;
-    T* __restrict__ oh = a.out_h + lofs;
+    const int rbase = max(y0 - NST, row_lo);
+    const int rtop = min(row_hi, y1 + NST + kU + kPf);  // past the last row the march loads
+    const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
+    const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
+    const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
+    const auto ru = make_rsrc(a.in_u + ib, in_bytes), rv = make_rsrc(a.in_v + ib, in_bytes),
+               rh = make_rsrc(a.in_h + ib, in_bytes);
+    const auto wu = make_rsrc(a.out_u + ob, out_bytes), wv = make_rsrc(a.out_v + ob, out_bytes),
+               wh = make_rsrc(a.out_h + ob, out_bytes);
+    const uint32_t row_bytes = (uint32_t)g.pitch * sizeof(T);
 
     const int xc = min(max(x, 0), g.W - 1);
+    const uint32_t loff = (uint32_t)xc * sizeof(T);
+    const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : 0x80000000u;
 #ifndef WS_ABLATE
 #define WS_ABLATE 0  // measurement builds only: 1 = no loads (compute only), 2 = no compute
 #endif
     auto load_row = [&](int R) -> V3<T> {
         const int r = min(max(R, row_lo), row_hi - 1);
-        const int64_t i = (int64_t)r * g.pitch + xc;
         if constexpr (WS_ABLATE == 1) {
             const T q = T(r & 7) * T(0.125) + T(xc & 3);
             return V3<T>{q, q * T(0.5), T(10) + q};
         } else {
-            return V3<T>{iu[i], iv[i], ih[i]};
+            const uint32_t so = (uint32_t)(r - rbase) * row_bytes;
+            return V3<T>{buf_load<T>(ru, loff, so), buf_load<T>(rv, loff, so), buf_load<T>(rh, loff, so)};
         }
     };
     auto store_row = [&](int j, const V3<T>& o) {
-        if (WS_ABLATE == 1 ? (xout && j >= y0 && j < y1 && o.u == T(12345.678)) : (xout && j >= y0 && j < y1)) {
-            const int64_t i = (int64_t)j * g.pitch + x;
-            __builtin_nontemporal_store(o.u, ou + i);
-            __builtin_nontemporal_store(o.v, ov + i);
-            __builtin_nontemporal_store(o.h, oh + i);
+        if (j >= y0 && j < y1) {
+            const uint32_t so = (uint32_t)(j - y0) * row_bytes;
+            const uint32_t vo = WS_ABLATE == 1 ? (o.u == T(12345.678) ? soff : 0x80000000u) : soff;
+            buf_store_nt<T>(o.u, wu, vo, so);
+            buf_store_nt<T>(o.v, wv, vo, so);
+            buf_store_nt<T>(o.h, wh, vo, so);
         }
     };
 
@@ -254,6 +289,10 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     if (nsegs <= 0) return hipSuccess;
     const int64_t nblocks = (int64_t)nstrips * nsegs * g.L;
     if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
+    // buffer descriptors span one segment's rows (+ margins); offsets are 32-bit and the
+    // dropped-store voffset is 2^31
+    const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 2 * kU + kPf) * g.pitch * (int64_t)sizeof(T);
+    if (span >= 0x7fffffff) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblocks), block(kWave);
     const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
 #define WS_DPP_LAUNCH(N)                                                                                   \
