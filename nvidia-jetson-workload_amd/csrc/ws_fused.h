@@ -36,4 +36,9 @@ constexpr int kDppCols = 64;
 template <typename T>
 hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
+// x2 variant: independent 64-lane waves, two adjacent columns per lane (128-column strips).
+int fused_x2_out_cols(int nstages);
+template <typename T>
+hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+
 }  // namespace ws

@@ -1,0 +1,114 @@
+// Device helpers shared by the wave-independent fused step kernels (ws_fused_dpp.hip,
+// ws_fused_x2.hip): buffer-descriptor memory access, DPP lane shifts, and the SWE
+// tendency written once for scalar and 2-wide (ext_vector) cell values.
+#pragma once
+
+#include "ws_fused.h"
+
+namespace ws {
+namespace dev {
+
+// ---- buffer descriptors: wave-uniform base (SGPRs) + 32-bit per-lane voffset ----------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+using U2 = unsigned int __attribute__((ext_vector_type(2)));
+using U4 = unsigned int __attribute__((ext_vector_type(4)));
+#ifndef WS_STORE_NT
+#define WS_STORE_NT 1
+#endif
+constexpr int kNT = WS_STORE_NT ? 2 : 0;  // cache policy bit: nontemporal (streamed output)
+constexpr uint32_t kDropped = 0x80000000u;  // voffset past every descriptor's range: op dropped
+
+// V is any 4-, 8- or 16-byte value type (float, double, float2, double2)
+template <typename V>
+__device__ __forceinline__ V buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    if constexpr (sizeof(V) == 16)
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+    else if constexpr (sizeof(V) == 8)
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+    else
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+template <typename V>
+__device__ __forceinline__ void buf_store_nt(V v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    if constexpr (sizeof(V) == 16)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)voff, (int)soff, kNT);
+    else if constexpr (sizeof(V) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, kNT);
+}
+
+// ---- DPP lane shifts -------------------------------------------------------------------
+// lane i <- lane i-1 (wave_shr:1) / lane i <- lane i+1 (wave_shl:1). Lanes without a source
+// read 0 (bound_ctrl): a strip's edge lanes, whose results lie in the discarded margin.
+// (Keeping the lane's own value instead costs a v_mov per shift to pre-load the destination.)
+__device__ __forceinline__ int shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int shl1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true); }
+
+__device__ __forceinline__ float from_left(float v) { return __builtin_bit_cast(float, shr1(__builtin_bit_cast(int, v))); }
+__device__ __forceinline__ float from_right(float v) { return __builtin_bit_cast(float, shl1(__builtin_bit_cast(int, v))); }
+__device__ __forceinline__ double from_left(double v) {
+    const U2 b = __builtin_bit_cast(U2, v);
+    U2 o;
+    o.x = (unsigned)shr1((int)b.x);
+    o.y = (unsigned)shr1((int)b.y);
+    return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double from_right(double v) {
+    const U2 b = __builtin_bit_cast(U2, v);
+    U2 o;
+    o.x = (unsigned)shl1((int)b.x);
+    o.y = (unsigned)shl1((int)b.y);
+    return __builtin_bit_cast(double, o);
+}
+
+// ---- the SWE tendency (weather_simulation.cpp:521-537), same evaluation order ---------
+// VT is T or a 2-wide ext_vector of T: every operation below is element-wise IEEE (the
+// build has -ffp-contract=off), so each element gets exactly the reference's arithmetic.
+template <typename VT>
+struct V3 {
+    VT u, v, h;
+};
+
+template <bool POW2, typename VT, typename T>
+__device__ __forceinline__ VT cdiff(VT ar, VT al, T two_d, T inv) {
+    if constexpr (POW2) return (ar - al) * inv;  // exact: inv is a power of two
+    else return (ar - al) / two_d;
+}
+
+template <bool POW2, typename VT, typename T>
+__device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V3<VT>& r, const V3<VT>& t,
+                                       const V3<VT>& b, const Spacing<T>& sp, T g, T f) {
+    const VT u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
+    const VT u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
+    const VT v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
+    const VT v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
+    const VT h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
+    const VT h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
+    V3<VT> k;
+    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
+    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
+    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
+    return k;
+}
+
+template <typename VT, typename T>
+__device__ __forceinline__ V3<VT> axpy(const V3<VT>& y, T c, const V3<VT>& k) {
+    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
+}
+
+// XCD-aware work mapping: consecutive work items (neighbouring strips of one segment,
+// which share halo columns) go to blocks b, b+8, ... that the dispatcher places on the
+// same XCD (same L2). Bijective for any block count. Speed only, never correctness.
+__device__ __forceinline__ int xcd_work_item() {
+    const int nb = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = nb / 8, rr = nb % 8, xcd = b % 8;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + b / 8;
+}
+
+}  // namespace dev
+}  // namespace ws

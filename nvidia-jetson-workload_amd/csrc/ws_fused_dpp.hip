@@ -63,7 +63,10 @@ __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
 }
 template <typename T>
 __device__ __forceinline__ void buf_store_nt(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    constexpr int kNT = 2;  // cache policy: nontemporal (streaming output, never re-read this step)
+#ifndef WS_STORE_NT
+#define WS_STORE_NT 1
+#endif
+    constexpr int kNT = WS_STORE_NT ? 2 : 0;  // cache policy: nontemporal (streamed output)
     if constexpr (sizeof(T) == 8) {
         using U2 = unsigned int __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
@@ -189,14 +192,17 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
             return V3<T>{buf_load<T>(ru, loff, so), buf_load<T>(rv, loff, so), buf_load<T>(rh, loff, so)};
         }
     };
+    // Stores are issued for every row, unconditionally: rows outside [y0, y1) are dropped by
+    // the range check through the voffset (a branch around them makes the compiler's vmcnt
+    // bookkeeping merge both paths and drain the load prefetch at every row).
     auto store_row = [&](int j, const V3<T>& o) {
-        if (j >= y0 && j < y1) {
-            const uint32_t so = (uint32_t)(j - y0) * row_bytes;
-            const uint32_t vo = WS_ABLATE == 1 ? (o.u == T(12345.678) ? soff : 0x80000000u) : soff;
-            buf_store_nt<T>(o.u, wu, vo, so);
-            buf_store_nt<T>(o.v, wv, vo, so);
-            buf_store_nt<T>(o.h, wh, vo, so);
-        }
+        const bool row_ok = j >= y0 && j < y1;
+        const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
+        uint32_t vo = row_ok ? soff : 0x80000000u;
+        if (WS_ABLATE == 1 && o.u != T(12345.678)) vo = 0x80000000u;
+        buf_store_nt<T>(o.u, wu, vo, so);
+        buf_store_nt<T>(o.v, wv, vo, so);
+        buf_store_nt<T>(o.h, wh, vo, so);
     };
 
     const V3<T> Z{T(0), T(0), T(0)};
@@ -210,8 +216,13 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 
     const int R0 = y0 - NST;
     const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
+    // prologue: each row followed by a (dropped) store row like every march body, so the
+    // loop is entered with the same outstanding-op pattern from here as from its back edge
 #pragma unroll
-    for (int i = 0; i < kPf; ++i) Y[i] = load_row(R0 + i);
+    for (int i = 0; i < kPf; ++i) {
+        Y[i] = load_row(R0 + i);
+        store_row(y0 - 1, Z);
+    }
 
     auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
         constexpr int P = decltype(Pc)::value;
@@ -220,6 +231,9 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        // keep the row's loads at the head of the body: the scheduler would otherwise sink
+        // them below the stencil math, shortening the prefetch distance
+        __builtin_amdgcn_sched_barrier(0);
         if constexpr (WS_ABLATE == 2) {
             store_row(R - NST, Y[yi(-NST)]);
             return;

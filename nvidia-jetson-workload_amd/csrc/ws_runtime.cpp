@@ -114,15 +114,21 @@ struct ws_grid {
 
 namespace {
 
+int64_t env_int(const char* name, int64_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoll(e) : dflt;
+}
+
 void grid_alloc(ws_grid* g, unsigned nfields) {
-    g->pitch = ((int64_t)g->W + 63) / 64 * 64;
+    g->pitch = ((int64_t)g->W + 63) / 64 * 64 + env_int("WS_PITCH_PAD", 0) / 64 * 64;
     g->lstride = ((int64_t)g->H + 2 * ws::kHalo) * g->pitch;
     g->nfields = nfields;
     const size_t es = elem_size(g->dtype);
+    const size_t stagger = (size_t)env_int("WS_FIELD_STAGGER", 0) / 256 * 256;  // bytes, field i offset by i*stagger
     for (unsigned i = 0; i < nfields; ++i) {
-        WS_HIP_CHECK(hipMalloc(&g->alloc[i], g->bytes_per_field()));
-        WS_HIP_CHECK(hipMemset(g->alloc[i], 0, g->bytes_per_field()));
-        g->f[i] = (char*)g->alloc[i] + (size_t)ws::kHalo * g->pitch * es;
+        WS_HIP_CHECK(hipMalloc(&g->alloc[i], g->bytes_per_field() + i * stagger));
+        WS_HIP_CHECK(hipMemset(g->alloc[i], 0, g->bytes_per_field() + i * stagger));
+        g->f[i] = (char*)g->alloc[i] + i * stagger + (size_t)ws::kHalo * g->pitch * es;
     }
 }
 
@@ -200,6 +206,8 @@ void convert(Dst* d, const Src* s, size_t n) {
 // ------------------------------------------------------------------------------------
 // simulation
 // ------------------------------------------------------------------------------------
+enum FusedKernel : int { kKernLds = 0, kKernDpp = 1, kKernX2 = 2 };
+
 struct ws_sim {
     ws_config_t cfg{};
     int32_t dtype = WS_F32;
@@ -225,8 +233,9 @@ struct ws_sim {
     bool own_stream = true;
     bool in_group = false;                              // a slab of a ws_group (local halo transport)
     bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
-    bool dpp = true;          // fused kernel variant: DPP waves (WS_KERNEL=dpp) or LDS workgroups (=lds)
+    int kernel = kKernX2;     // fused kernel variant (WS_KERNEL=x2|dpp|lds)
     int32_t seg_override = 0; // WS_SEG_ROWS
+    int32_t want_blocks_override = 0;  // WS_WANT_BLOCKS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
     int32_t row0 = 0;
@@ -236,8 +245,11 @@ struct ws_sim {
     int32_t seg_rows(int nst) const {
         if (seg_override > 0) return seg_override;
         const ws_grid* g = slot[0];
-        const int out_w = (dpp ? ws::kDppCols : ws::kFusedCols) - 2 * nst;
-        const int64_t want_blocks = dpp ? 4096 : 512;  // 64-lane vs 256-lane workgroups
+        const int out_w = kernel == kKernX2 ? ws::fused_x2_out_cols(nst)
+                          : (kernel == kKernDpp ? ws::kDppCols : ws::kFusedCols) - 2 * nst;
+        // 64-lane waves of 128 / 64 columns vs 256-lane workgroups
+        int64_t want_blocks = kernel == kKernX2 ? 2048 : kernel == kKernDpp ? 4096 : 512;
+        if (want_blocks_override > 0) want_blocks = want_blocks_override;
         const int64_t strips = (g->W + out_w - 1) / out_w;
         const int64_t want_segs = std::max<int64_t>(1, (want_blocks + strips * g->L - 1) / (strips * g->L));
         int64_t rows = (g->H + want_segs - 1) / want_segs;
@@ -330,8 +342,11 @@ void fused_launch(ws_sim* s, int nst, int segA, int nA, int segB, int nB) {
     a.seg_b = segB;
     a.seg_n = nA + nB;
     const ws::Geom g = c->geom();
-    WS_HIP_CHECK(s->dpp ? ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)
-                        : ws::launch_fused_step<T>(nst, a, g, s->stream));
+    switch (s->kernel) {
+        case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, s->stream)); break;
+        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)); break;
+        default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, s->stream)); break;
+    }
     ++s->last_launches;
 }
 
@@ -526,7 +541,9 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
-        if (const char* e = std::getenv("WS_KERNEL")) s->dpp = std::strcmp(e, "lds") != 0;
+        if (const char* e = std::getenv("WS_KERNEL"))
+            s->kernel = std::strcmp(e, "lds") == 0 ? kKernLds : std::strcmp(e, "dpp") == 0 ? kKernDpp : kKernX2;
+        if (const char* e = std::getenv("WS_WANT_BLOCKS")) s->want_blocks_override = std::atoi(e);
         if (const char* e = std::getenv("WS_SEG_ROWS")) s->seg_override = std::atoi(e);
         const int method = effective_method(*cfg);
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);

@@ -1,0 +1,51 @@
+"""Column-pair ("x2") fused kernel edge cases, bitwise vs the CPU oracle: odd widths (the
+last pair straddles x = W-1), widths narrower than one 128-column strip, widths that end
+exactly on a strip boundary, and non-power-of-two spacing (IEEE-divide instantiation)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ws = pytest.importorskip("weather_sim")
+if not ws.is_cuda_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+
+def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3):
+    from oracle.ws_oracle import OracleSim
+
+    c = ws.SimulationConfig()
+    c.grid_width, c.grid_height = W, H
+    c.integration_method, c.double_precision = method, fp64
+    c.dx, c.dy, c.coriolis_f = dx, dy, f
+    sim = ws.WeatherSimulation(c)
+    sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
+    sim.initialize()
+    g = sim.get_current_grid()
+    ref = OracleSim(W, H, 0, method, dx=dx, dy=dy, coriolis_f=f, precision="f64" if fp64 else "f32")
+    ref.initialize()
+    u, v = g.get_velocity_field()
+    for k, a in (("u", u), ("v", v), ("h", g.get_height_field())):
+        ref.set_field(k, a)
+    sim.run(steps)
+    ref.run(steps)
+    g = sim.get_current_grid()
+    u, v = g.get_velocity_field()
+    got = {"u": u, "v": v, "h": g.get_height_field(), "vort": g.get_vorticity_field()}
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=f"W={W} {k}")
+
+
+@pytest.mark.parametrize("W", [2, 3, 7, 64, 120, 121, 127, 128, 129, 240, 241, 333])
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_x2_widths(W, method, fp64, monkeypatch):
+    monkeypatch.setenv("WS_KERNEL", "x2")
+    monkeypatch.setenv("WS_SEG_ROWS", "7")
+    run_both(W, 29, method, fp64, 5)
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_x2_non_pow2(method, monkeypatch):
+    monkeypatch.setenv("WS_KERNEL", "x2")
+    run_both(301, 40, method, True, 4, dx=0.75, dy=1.3)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build an A/B measurement variant of libws_hip.so with extra -D flags on the DPP kernel:
+#   tools/variant.sh NAME "-DWS_DPP_PF=5 ..."   -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
+set -eu
+cd "$(dirname "$0")/../nvidia-jetson-workload_amd/csrc"
+make -s -j8 >/dev/null
+NAME=$1; DEFS=${2:-}; SRC=${3:-ws_fused_dpp.hip}
+mkdir -p _obj/var ../lib/variants
+FLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include -I/opt/rocm/include"
+/opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/$NAME.o
+OBJS=$(ls _obj/*.o | grep -v "/${SRC}.o$")
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/variants/libws_hip_$NAME.so $OBJS _obj/var/$NAME.o \
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+echo "built lib/variants/libws_hip_$NAME.so"
