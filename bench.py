@@ -194,6 +194,7 @@ def main():
     cells = conf["W"] * conf["H"] * conf["L"]
     value = cells * args.steps / elapsed
     stats = sim.kernel_timing()
+    variant, seg_rows = sim.fused_variant()
     dev_ms, launches = sim.last_run_stats()
     # dominant kernel = largest total device time
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
@@ -222,7 +223,8 @@ def main():
                    "parallelism": f"y-slab x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"stage{kind}", "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n},
+                     "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
+                     "seg_rows": seg_rows, "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
         "kernel_stats": {f"stage{k}": {"launches": v[0], "mean_ms": v[1] / v[0], "bytes": v[2],
                                        "gbs": v[2] / (v[1] / v[0] * 1e-3) / 1e9} for k, v in stats.items()},

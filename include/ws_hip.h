@@ -240,6 +240,12 @@ int ws_sim_set_kernel_timing(ws_sim_t* sim, int32_t enable);
 int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, double* total_ms,
                          double* bytes_per_launch);
 
+/* The fused step-kernel variant in use: kernel 0 = LDS workgroups, 1 = DPP waves (64
+ * columns per wave), 2 = column pairs (128 columns per wave), -1 = per-stage kernels;
+ * seg_rows = output rows per segment. Chosen by timing every variant on the real grid at
+ * the first run (all are bit-identical), unless WS_KERNEL / WS_SEG_ROWS fix it. */
+int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows);
+
 #ifdef __cplusplus
 }
 #endif

@@ -233,8 +233,10 @@ struct ws_sim {
     bool own_stream = true;
     bool in_group = false;                              // a slab of a ws_group (local halo transport)
     bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
-    int kernel = kKernX2;     // fused kernel variant (WS_KERNEL=x2|dpp|lds)
-    int32_t seg_override = 0; // WS_SEG_ROWS
+    int kernel = kKernDpp;    // fused kernel variant (WS_KERNEL=x2|dpp|lds fixes it)
+    int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
+    bool kernel_fixed = false, seg_fixed = false;
+    bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
     int32_t want_blocks_override = 0;  // WS_WANT_BLOCKS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
@@ -455,9 +457,63 @@ int plan_steps(const ws_sim* s, int n) {
     return k;
 }
 
+// Pick the fused-kernel variant (and segment length) for this grid by timing each
+// candidate on the real fields once, at the first run: all variants produce bit-identical
+// results (each is the reference's arithmetic), they differ only in speed, and which is
+// fastest depends on precision, integrator, width and level count. A candidate launch
+// reads the current state and writes the next-state buffer, which the real step then
+// overwrites, so tuning leaves no trace in the results.
+template <typename T>
+void autotune(ws_sim* s) {
+    s->tuned = true;
+    if (!use_fused(s) || s->kernel_fixed || s->in_group) return;
+    const int nst = fused_stages(s);
+    struct Cand {
+        int kernel, seg;
+        float ms;
+    };
+    std::vector<Cand> cands;
+    for (int k : {kKernDpp, kKernX2, kKernLds}) {
+        cands.push_back({k, s->seg_fixed ? s->seg_override : 0, 0.f});
+        if (!s->seg_fixed) {
+            s->kernel = k;
+            s->seg_override = 0;
+            const int d = s->seg_rows(nst);
+            const int half = ((d + 2 * nst) / 2 + 7) / 8 * 8 - 2 * nst;  // ~half, unroll-aligned march
+            if (half >= 6 * nst && half < d) cands.push_back({k, half, 0.f});
+        }
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    WS_HIP_CHECK(hipEventCreate(&e0));
+    WS_HIP_CHECK(hipEventCreate(&e1));
+    for (Cand& c : cands) {
+        s->kernel = c.kernel;
+        s->seg_override = c.seg;
+        const int nsegs = seg_split(s, nst).nsegs;
+        fused_launch<T>(s, nst, 0, nsegs, 0, 0);  // warm (code load, caches)
+        WS_HIP_CHECK(hipEventRecord(e0, s->stream));
+        for (int i = 0; i < 3; ++i) fused_launch<T>(s, nst, 0, nsegs, 0, 0);
+        WS_HIP_CHECK(hipEventRecord(e1, s->stream));
+        WS_HIP_CHECK(hipEventSynchronize(e1));
+        WS_HIP_CHECK(hipEventElapsedTime(&c.ms, e0, e1));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    const Cand* best = &cands[0];
+    for (const Cand& c : cands)
+        if (c.ms < best->ms) best = &c;
+    s->kernel = best->kernel;
+    s->seg_override = best->seg;
+    s->last_launches = 0;
+}
+
 void run_steps(ws_sim* s, int k) {
     require(!s->in_group, WS_ERR_INVALID, "a slab of a group steps only with ws_group_run");
     set_device(s->device);
+    if (!s->tuned && k > 0) {
+        if (s->dtype == WS_F64) autotune<double>(s);
+        else autotune<float>(s);
+    }
     s->last_launches = 0;
     WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
     for (int i = 0; i < k; ++i) {
@@ -541,10 +597,16 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
-        if (const char* e = std::getenv("WS_KERNEL"))
+        if (const char* e = std::getenv("WS_KERNEL")) {
             s->kernel = std::strcmp(e, "lds") == 0 ? kKernLds : std::strcmp(e, "dpp") == 0 ? kKernDpp : kKernX2;
+            s->kernel_fixed = true;
+        }
         if (const char* e = std::getenv("WS_WANT_BLOCKS")) s->want_blocks_override = std::atoi(e);
-        if (const char* e = std::getenv("WS_SEG_ROWS")) s->seg_override = std::atoi(e);
+        if (const char* e = std::getenv("WS_SEG_ROWS")) {
+            s->seg_override = std::atoi(e);
+            s->seg_fixed = s->seg_override > 0;
+        }
+        if (const char* e = std::getenv("WS_AUTOTUNE")) s->tuned = std::atoi(e) == 0;
         const int method = effective_method(*cfg);
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
         if (!s->fused && method == WS_RK4) {
@@ -1144,6 +1206,15 @@ int ws_sim_kernel_timing(const ws_sim_t* s, int32_t kind, int64_t* launches, dou
         if (launches) *launches = st.launches;
         if (total_ms) *total_ms = st.total_ms;
         if (bytes_per_launch) *bytes_per_launch = st.bytes_per_launch;
+    });
+}
+
+int ws_sim_fused_variant(const ws_sim_t* s, int32_t* kernel, int32_t* seg_rows) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        const bool fused = use_fused(s);
+        if (kernel) *kernel = fused ? s->kernel : -1;
+        if (seg_rows) *seg_rows = fused ? s->seg_rows(fused_stages(s)) : 0;
     });
 }
 

@@ -667,6 +667,12 @@ class WeatherSimulation:
                 out[k] = (n.value, ms.value, b.value)
         return out
 
+    def fused_variant(self):
+        """(kernel name, rows per segment) of the fused step kernel in use (after the first run)."""
+        k, seg = ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg)))
+        return {-1: "stage_kernels", 0: "fused_lds", 1: "fused_dpp", 2: "fused_x2"}[k.value], seg.value
+
     def comm_allreduce_max(self, value):
         out = ctypes.c_double()
         check(lib.ws_sim_comm_allreduce_max(self._h, float(value), ctypes.byref(out)))
