@@ -486,17 +486,25 @@ void autotune(ws_sim* s) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     WS_HIP_CHECK(hipEventCreate(&e0));
     WS_HIP_CHECK(hipEventCreate(&e1));
-    for (Cand& c : cands) {
+    // round-robin rounds, best-of per candidate: robust to clock ramp-up and noise
+    auto time_cand = [&](Cand& c, int reps) {
         s->kernel = c.kernel;
         s->seg_override = c.seg;
         const int nsegs = seg_split(s, nst).nsegs;
-        fused_launch<T>(s, nst, 0, nsegs, 0, 0);  // warm (code load, caches)
         WS_HIP_CHECK(hipEventRecord(e0, s->stream));
-        for (int i = 0; i < 3; ++i) fused_launch<T>(s, nst, 0, nsegs, 0, 0);
+        for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, 0, nsegs, 0, 0);
         WS_HIP_CHECK(hipEventRecord(e1, s->stream));
         WS_HIP_CHECK(hipEventSynchronize(e1));
-        WS_HIP_CHECK(hipEventElapsedTime(&c.ms, e0, e1));
-    }
+        float ms = 0.f;
+        WS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        return ms / reps;
+    };
+    float first = 0.f;
+    for (Cand& c : cands) first += time_cand(c, 1);  // warm-up (code load, clocks)
+    const int reps = (int)std::clamp(10.0f * (float)cands.size() / std::max(first, 1e-3f), 2.0f, 8.0f);
+    for (Cand& c : cands) c.ms = 1e30f;
+    for (int round = 0; round < 3; ++round)
+        for (Cand& c : cands) c.ms = std::min(c.ms, time_cand(c, reps));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     const Cand* best = &cands[0];

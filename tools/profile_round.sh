@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round profile of the bench workload: bench (autotuned) -> rocprofv3 kernel-trace stats and
+# PMC passes with the variant the autotuner chose pinned (so every profiled dispatch of the
+# kernel is the measured one) -> traffic JSON. Outputs under gpurun_out/round/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+OUT=$R/gpurun_out/round
+mkdir -p "$OUT/pmc"
+CFG=${CFG:-c2}; METHOD=${METHOD:-rk4}; STEPS=${STEPS:-50}; WARM=${WARM:-10}
+timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS --warmup $WARM > "$OUT/bench.json" 2> "$OUT/bench.err"
+rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
+read KERN SEG < <(python3 -c "
+import json; d=json.load(open('$OUT/bench.json'))['roofline']
+print({'fused_dpp':'dpp','fused_x2':'x2','fused_lds':'lds'}.get(d['kernel'],'dpp'), d.get('seg_rows') or 0)")
+echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG"
+export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
+      python3 "$R/bench.py" --config $CFG --method $METHOD --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/pmc/p$i.log" 2>&1
+  rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc/p$i.log"; exit $rc; }
+done
+python3 "$R/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc_summary.txt"
+python3 "$R/tools/traffic.py" "$OUT/pmc" "fused_${KERN}_kernel" "$OUT/traffic_${CFG}_${METHOD}.json"
