@@ -79,6 +79,14 @@ def max_over_ranks(dist, seconds):
     return float(t[0])
 
 
+def stagewise_words(model, method):
+    """SURVEY §8(d) words per cell-update of a stage-by-stage step (non-SWE RK4 runs RK2,
+    AB / semi-implicit run Euler: weather_simulation.cpp:117-158, 334-338)."""
+    if method == 2 and model != 0:
+        method = 1
+    return {0: 6, 1: 15, 2: 45}.get(method, 6)
+
+
 def cpu_baseline(conf, method, budget_s=20.0):
     """Time the reference CPU solver (or the oracle port) on a bounded sample."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -226,6 +234,10 @@ def main():
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
                      "seg_rows": seg_rows, "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
+        # SURVEY §8(d) prices the path as stage-by-stage passes (Euler 6w, RK2 15w, RK4 45w per
+        # cell): the rate that traffic would need at the measured launch time
+        "equivalent_stagewise_gbs": (stagewise_words(conf["model"], method) * (8 if conf["fp64"] else 4) * cells
+                                     / (tot_ms / n * 1e-3) / 1e9) if variant != "stage_kernels" else None,
         "kernel_stats": {f"stage{k}": {"launches": v[0], "mean_ms": v[1] / v[0], "bytes": v[2],
                                        "gbs": v[2] / (v[1] / v[0] * 1e-3) / 1e9} for k, v in stats.items()},
     }
