@@ -44,6 +44,13 @@ CONFIGS = {
                workload="C4: Primitive Equations (reference semantics) 1024x1024x32 levels fp32"),
     "c5": dict(W=16384, H=16384, L=1, model=0, fp64=True, ic="jet_stream",
                workload="C5: Shallow Water 16384x16384 fp64"),
+    # one rank's share of C2 at 2 / 4 / 8 GPUs (measurement aid for the strong-scaling budget)
+    "c2_slab2": dict(W=4096, H=2048, L=1, model=0, fp64=True, ic="jet_stream",
+                     workload="C2 slab of 2: Shallow Water 4096x2048 fp64"),
+    "c2_slab4": dict(W=4096, H=1024, L=1, model=0, fp64=True, ic="jet_stream",
+                     workload="C2 slab of 4: Shallow Water 4096x1024 fp64"),
+    "c2_slab8": dict(W=4096, H=512, L=1, model=0, fp64=True, ic="jet_stream",
+                     workload="C2 slab of 8: Shallow Water 4096x512 fp64"),
 }
 METHODS = {"euler": 0, "rk2": 1, "rk4": 2}
 

@@ -19,8 +19,10 @@ constexpr int kWave = 64;
 #ifndef WS_DPP_PF
 #define WS_DPP_PF 3
 #endif
-constexpr int kPf = WS_DPP_PF;             // rows of y loads in flight per lane
-constexpr int kU = (5 + kPf + 1) / 2 * 2;  // march unroll = y ring length (>= 5 past rows + kPf, even)
+// rows of y loads in flight per lane (template parameter PF; 3 measured best at C2 -- a
+// 6-row variant did not help even on grids too small to fill the chip)
+constexpr int unroll_for(int pf) { return (5 + pf + 1) / 2 * 2; }  // y ring length (>= 5 past rows + pf, even)
+constexpr int kUMax = unroll_for(WS_DPP_PF);
 
 template <typename T>
 struct V3 {
@@ -131,9 +133,11 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
 #define WS_DPP_MINW 1
 #endif
 
-template <typename T, int NST, bool POW2>
+template <typename T, int NST, bool POW2, int PF>
 __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
+    constexpr int kPf = PF;
+    constexpr int kU = unroll_for(PF);
     constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
     static_assert(kYb + kPf <= kU, "y ring too short");
 
@@ -305,13 +309,14 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
     // buffer descriptors span one segment's rows (+ margins); offsets are 32-bit and the
     // dropped-store voffset is 2^31
-    const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 2 * kU + kPf) * g.pitch * (int64_t)sizeof(T);
+    const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 3 * kUMax) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblocks), block(kWave);
     const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
-#define WS_DPP_LAUNCH(N)                                                                                   \
-    if (pow2) hipLaunchKernelGGL((fused_dpp_kernel<T, N, true>), grid, block, 0, s, a, g, nstrips, nsegs);  \
-    else hipLaunchKernelGGL((fused_dpp_kernel<T, N, false>), grid, block, 0, s, a, g, nstrips, nsegs);
+#define WS_DPP_GO(N, P2, PF) hipLaunchKernelGGL((fused_dpp_kernel<T, N, P2, PF>), grid, block, 0, s, a, g, nstrips, nsegs)
+#define WS_DPP_LAUNCH(N)              \
+    if (pow2) WS_DPP_GO(N, true, WS_DPP_PF); \
+    else WS_DPP_GO(N, false, WS_DPP_PF);
     switch (nstages) {
         case 1: WS_DPP_LAUNCH(1) break;
         case 2: WS_DPP_LAUNCH(2) break;
@@ -319,6 +324,7 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
         default: return hipErrorInvalidValue;
     }
 #undef WS_DPP_LAUNCH
+#undef WS_DPP_GO
     return hipGetLastError();
 }
 

@@ -242,22 +242,30 @@ struct ws_sim {
     ws::SlabComm* comm = nullptr;
     int32_t row0 = 0;
 
-    // Rows per fused-kernel segment: enough workgroups for ~2 per CU (256 CUs), but
-    // segments long enough that the 2*NST warm-up rows stay a small overhead.
-    int32_t seg_rows(int nst) const {
-        if (seg_override > 0) return seg_override;
-        const ws_grid* g = slot[0];
+    int64_t strips(int nst) const {
         const int out_w = kernel == kKernX2 ? ws::fused_x2_out_cols(nst)
                           : (kernel == kKernDpp ? ws::kDppCols : ws::kFusedCols) - 2 * nst;
-        // 64-lane waves of 128 / 64 columns vs 256-lane workgroups
+        return (slot[0]->W + out_w - 1) / out_w;
+    }
+    // segment rows giving about want_blocks workgroups (at least min_rows rows; the march
+    // length rows + 2 NST a multiple of the unroll)
+    int32_t seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const {
+        const ws_grid* g = slot[0];
+        const int64_t per_seg = strips(nst) * g->L;
+        const int64_t want_segs = std::max<int64_t>(1, (want_blocks + per_seg - 1) / per_seg);
+        int64_t rows = (g->H + want_segs - 1) / want_segs;
+        rows = std::max<int64_t>(rows, min_rows);
+        rows = (rows + 2 * nst + 7) / 8 * 8 - 2 * nst;
+        return (int32_t)std::max<int64_t>(1, std::min<int64_t>(rows, g->H));
+    }
+    // Rows per fused-kernel segment: enough workgroups to fill the chip (64-lane waves of
+    // 64 / 128 columns vs 256-lane workgroups), segments long enough that the 2*NST
+    // warm-up rows stay a small overhead. The autotuner also tries other counts.
+    int32_t seg_rows(int nst) const {
+        if (seg_override > 0) return seg_override;
         int64_t want_blocks = kernel == kKernX2 ? 2048 : kernel == kKernDpp ? 4096 : 512;
         if (want_blocks_override > 0) want_blocks = want_blocks_override;
-        const int64_t strips = (g->W + out_w - 1) / out_w;
-        const int64_t want_segs = std::max<int64_t>(1, (want_blocks + strips * g->L - 1) / (strips * g->L));
-        int64_t rows = (g->H + want_segs - 1) / want_segs;
-        rows = std::max<int64_t>(rows, 24 * nst);
-        rows = (rows + 2 * nst + 7) / 8 * 8 - 2 * nst;  // march length (rows + 2 NST) a multiple of the unroll
-        return (int32_t)std::max<int64_t>(1, std::min<int64_t>(rows, g->H));
+        return seg_for_blocks(nst, want_blocks, 24 * nst);
     }
 };
 
@@ -474,14 +482,21 @@ void autotune(ws_sim* s) {
     };
     std::vector<Cand> cands;
     for (int k : {kKernDpp, kKernX2, kKernLds}) {
-        cands.push_back({k, s->seg_fixed ? s->seg_override : 0, 0.f});
-        if (!s->seg_fixed) {
-            s->kernel = k;
-            s->seg_override = 0;
-            const int d = s->seg_rows(nst);
-            const int half = ((d + 2 * nst) / 2 + 7) / 8 * 8 - 2 * nst;  // ~half, unroll-aligned march
-            if (half >= 6 * nst && half < d) cands.push_back({k, half, 0.f});
+        s->kernel = k;
+        s->seg_override = 0;
+        if (s->seg_fixed) {
+            cands.push_back({k, s->seg_override, 0.f});
+            continue;
         }
+        // the default, and segment lengths giving whole multiples of the chip's wave slots
+        // (1024 SIMDs; an LDS workgroup is 4 waves) so no SIMD runs a lone extra wave
+        std::vector<int> segs{s->seg_rows(nst)};
+        const int wave_per_block = k == kKernLds ? 4 : 1;
+        for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
+            segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
+        std::sort(segs.begin(), segs.end());
+        segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
+        for (int seg : segs) cands.push_back({k, seg, 0.f});
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     WS_HIP_CHECK(hipEventCreate(&e0));

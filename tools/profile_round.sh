@@ -10,9 +10,11 @@ mkdir -p "$OUT/pmc"
 CFG=${CFG:-c2}; METHOD=${METHOD:-rk4}; STEPS=${STEPS:-50}; WARM=${WARM:-10}
 timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS --warmup $WARM > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
-read KERN SEG < <(python3 -c "
+read KERN KNAME SEG < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
-print({'fused_dpp':'dpp','fused_x2':'x2','fused_lds':'lds'}.get(d['kernel'],'dpp'), d.get('seg_rows') or 0)")
+k={'fused_dpp':'dpp','fused_dppdeep':'dppdeep','fused_x2':'x2','fused_lds':'lds'}.get(d['kernel'],'dpp')
+n={'dpp':'fused_dpp_kernel','dppdeep':'fused_dpp_kernel','x2':'fused_x2_kernel','lds':'fused_step_kernel'}[k]
+print(k, n, d.get('seg_rows') or 0)")
 echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG"
 export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG
 cd /tmp && export TMPDIR=/tmp
@@ -28,4 +30,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
   rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc/p$i.log"; exit $rc; }
 done
 python3 "$R/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc_summary.txt"
-python3 "$R/tools/traffic.py" "$OUT/pmc" "fused_${KERN}_kernel" "$OUT/traffic_${CFG}_${METHOD}.json"
+python3 "$R/tools/traffic.py" "$OUT/pmc" "$KNAME" "$OUT/traffic_${CFG}_${METHOD}.json"
