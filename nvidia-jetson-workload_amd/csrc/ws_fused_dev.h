@@ -15,6 +15,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 
 using U2 = unsigned int __attribute__((ext_vector_type(2)));
 using U4 = unsigned int __attribute__((ext_vector_type(4)));
+#ifndef WS_SCHED_BARRIER
+#define WS_SCHED_BARRIER 1  // pin each row's loads at the head of the march body
+#endif
 #ifndef WS_STORE_NT
 #define WS_STORE_NT 1
 #endif

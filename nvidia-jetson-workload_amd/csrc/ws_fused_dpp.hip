@@ -9,11 +9,14 @@
 // Arithmetic per cell is the reference's, in the reference's order
 // (weather_simulation.cpp:160-455, 473-540): results are bit-for-bit those of the CPU solver.
 #include <type_traits>
+#include <utility>
 
-#include "ws_fused.h"
+#include "ws_fused_dev.h"
 
 namespace ws {
 namespace {
+
+using namespace dev;
 
 constexpr int kWave = 64;
 #ifndef WS_DPP_PF
@@ -23,87 +26,6 @@ constexpr int kWave = 64;
 // 6-row variant did not help even on grids too small to fill the chip)
 constexpr int unroll_for(int pf) { return (5 + pf + 1) / 2 * 2; }  // y ring length (>= 5 past rows + pf, even)
 constexpr int kUMax = unroll_for(WS_DPP_PF);
-
-template <typename T>
-struct V3 {
-    T u, v, h;
-};
-
-// lane i <- lane i-1 (value of the left column) / lane i <- lane i+1 (right column).
-// Lanes without a source read 0 (bound_ctrl): they are a strip's edge lanes, whose results
-// lie in the discarded NST-lane margin. (Keeping the lane's own value instead would cost a
-// v_mov per DPP to pre-load the destination: 48 VALU per row in fp64 RK4.)
-__device__ __forceinline__ int dpp_from_left(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
-__device__ __forceinline__ int dpp_from_right(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true); }
-
-__device__ __forceinline__ float from_left(float v) {
-    return __builtin_bit_cast(float, dpp_from_left(__builtin_bit_cast(int, v)));
-}
-__device__ __forceinline__ float from_right(float v) {
-    return __builtin_bit_cast(float, dpp_from_right(__builtin_bit_cast(int, v)));
-}
-__device__ __forceinline__ double from_left(double v) {
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = dpp_from_left((int)b), hi = dpp_from_left((int)(b >> 32));
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ double from_right(double v) {
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = dpp_from_right((int)b), hi = dpp_from_right((int)(b >> 32));
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-template <typename T>
-__device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    if constexpr (sizeof(T) == 8)
-        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
-    else
-        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
-}
-template <typename T>
-__device__ __forceinline__ void buf_store_nt(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-#ifndef WS_STORE_NT
-#define WS_STORE_NT 1
-#endif
-    constexpr int kNT = WS_STORE_NT ? 2 : 0;  // cache policy: nontemporal (streamed output)
-    if constexpr (sizeof(T) == 8) {
-        using U2 = unsigned int __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, kNT);
-    }
-}
-
-template <bool POW2, typename T>
-__device__ __forceinline__ T cdiff(T ar, T al, T two_d, T inv) {
-    if constexpr (POW2) return (ar - al) * inv;
-    else return (ar - al) / two_d;
-}
-
-// SWE tendency (weather_simulation.cpp:521-537), same evaluation order.
-template <bool POW2, typename T>
-__device__ __forceinline__ V3<T> tend(const V3<T>& c, const V3<T>& l, const V3<T>& r, const V3<T>& t,
-                                      const V3<T>& b, const Spacing<T>& sp, T g, T f) {
-    const T u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
-    const T u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
-    const T v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
-    const T v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
-    const T h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
-    const T h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
-    V3<T> k;
-    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
-    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
-    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
-    return k;
-}
-
-template <typename T>
-__device__ __forceinline__ V3<T> axpy(const V3<T>& y, T c, const V3<T>& k) {
-    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
-}
 
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
 // XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
@@ -141,13 +63,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
     static_assert(kYb + kPf <= kU, "y ring too short");
 
-    // XCD-aware work mapping: consecutive work items (neighbouring strips of one segment,
-    // which share halo columns) go to blocks b, b+8, ... that the dispatcher places on the
-    // same XCD (same L2). Bijective for any block count. Speed only, never correctness.
-    const int nb = gridDim.x;
-    const int b = blockIdx.x;
-    const int q = nb / 8, rr = nb % 8, xcd = b % 8;
-    const int w = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + b / 8;
+    const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
     const int seg = fused_segment((w / nstrips) % nsegs, a.seg_a, a.seg_na, a.seg_b);
     const int level = w / (nstrips * nsegs);
@@ -182,7 +98,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 
     const int xc = min(max(x, 0), g.W - 1);
     const uint32_t loff = (uint32_t)xc * sizeof(T);
-    const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : 0x80000000u;
+    const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : kDropped;
 #ifndef WS_ABLATE
 #define WS_ABLATE 0  // measurement builds only: 1 = no loads (compute only), 2 = no compute
 #endif
@@ -202,8 +118,8 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     auto store_row = [&](int j, const V3<T>& o) {
         const bool row_ok = j >= y0 && j < y1;
         const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
-        uint32_t vo = row_ok ? soff : 0x80000000u;
-        if (WS_ABLATE == 1 && o.u != T(12345.678)) vo = 0x80000000u;
+        uint32_t vo = row_ok ? soff : kDropped;
+        if (WS_ABLATE == 1 && o.u != T(12345.678)) vo = kDropped;
         buf_store_nt<T>(o.u, wu, vo, so);
         buf_store_nt<T>(o.v, wv, vo, so);
         buf_store_nt<T>(o.h, wh, vo, so);
@@ -228,18 +144,31 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         store_row(y0 - 1, Z);
     }
 
-    auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
+    // Warm-up (the first kU bodies of a segment, Wc = true): stage s at row R - s is needed
+    // for the segment's outputs only from R - R0 >= 2s on (its cone above y0 is NST - s rows
+    // deep), so earlier bodies skip it -- NST(NST+1) stage-rows less per segment (RK4: 20).
+    // A skipped final stage still issues its (dropped) store row, keeping every body's
+    // load/store pattern identical for the compiler's vmcnt bookkeeping.
+    auto body = [&](auto Pc, auto Xc, auto Yc, auto Wc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
         constexpr bool YC = decltype(Yc)::value;
+        constexpr bool WARM = decltype(Wc)::value;
+        constexpr auto on = [](int st) { return !WARM || P >= 2 * st; };
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
         // keep the row's loads at the head of the body: the scheduler would otherwise sink
         // them below the stencil math, shortening the prefetch distance
+#if WS_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
         if constexpr (WS_ABLATE == 2) {
             store_row(R - NST, Y[yi(-NST)]);
+            return;
+        }
+        if constexpr (!on(1)) {
+            store_row(y0 - 1, Z);
             return;
         }
         const V3<T> k1 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1,
@@ -248,42 +177,56 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
             store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
         } else {
             const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
-            const V3<T> k2 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
-                                                      a.gravity, a.coriolis_f);
-            S1[r2(-1)] = s1;
-            if constexpr (NST == 2) {
-                store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+            if constexpr (on(2)) {
+                const V3<T> k2 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
+                                                          a.gravity, a.coriolis_f);
+                if constexpr (NST == 2) {
+                    store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+                } else {
+                    const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                    if constexpr (on(3)) {
+                        const V3<T> k3 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2,
+                                                                  a.sp2, a.gravity, a.coriolis_f);
+                        const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
+                        if constexpr (on(4)) {
+                            const V3<T> k4 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 4, g, S3[r2(-5)], S3[r2(-4)],
+                                                                      s3, a.sp2, a.gravity, a.coriolis_f);
+                            // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                            const T two = T(2);
+                            const V3<T>& y4 = Y[yi(-4)];
+                            const V3<T>& kk2 = K2[r2(-4)];
+                            const V3<T>& kk3 = K3[r2(-4)];
+                            V3<T> o;
+                            o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
+                            o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
+                            o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                            store_row(R - 4, o);
+                        } else {
+                            store_row(y0 - 1, Z);
+                        }
+                        S3[r2(-3)] = s3;  // after k4 read S3[r2(-5)] (same slot)
+                        K3[r2(-3)] = k3;
+                    } else {
+                        store_row(y0 - 1, Z);
+                    }
+                    S2[r2(-2)] = s2;  // after k3 read S2[r2(-4)] (same slot)
+                    K2[r2(-2)] = k2;  // after the final combination read K2[r2(-4)]
+                }
             } else {
-                const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
-                const V3<T> k3 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
-                                                          a.gravity, a.coriolis_f);
-                const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
-                const V3<T> k4 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3, a.sp2,
-                                                          a.gravity, a.coriolis_f);
-                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
-                const T two = T(2);
-                const V3<T>& y4 = Y[yi(-4)];
-                const V3<T>& kk2 = K2[r2(-4)];
-                const V3<T>& kk3 = K3[r2(-4)];
-                V3<T> o;
-                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
-                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
-                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
-                store_row(R - 4, o);
-                S2[r2(-2)] = s2;
-                S3[r2(-3)] = s3;
-                K2[r2(-2)] = k2;
-                K3[r2(-3)] = k3;
+                store_row(y0 - 1, Z);
             }
+            S1[r2(-1)] = s1;  // after k2 read S1[r2(-3)] (same slot)
         }
     };
 
     auto march = [&](auto Xc, auto Yc) {
-        for (int R = R0; R < R1; R += kU) {
+        auto period = [&](auto Wc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-                (body(std::integral_constant<int, Ps>{}, Xc, Yc, R + Ps), ...);
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, Wc, R + Ps), ...);
             }(std::make_integer_sequence<int, kU>{});
-        }
+        };
+        period(std::true_type{}, R0);  // R1 - R0 >= kU: the march spans >= 2 NST rows
+        for (int R = R0 + kU; R < R1; R += kU) period(std::false_type{}, R);
     };
     // global edges matter only to strips / segments within NST cells of them
     const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - NST;

@@ -199,7 +199,9 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
         Y[yi(kPf)] = load_row(Xc, R + kPf);  // its slot held row R + kPf - kNY: dead
         // keep the row's loads at the head of the body: the scheduler would otherwise sink
         // them below the stencil math, shortening the prefetch distance
+#if WS_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
 #ifdef WS_ABLATE
         if constexpr (WS_ABLATE == 2) {  // measurement build: memory stream only, no stencil math
             store_row(Xc, R - NST, Y[yi(-NST < -2 ? -2 : -NST)]);

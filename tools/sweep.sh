@@ -9,7 +9,7 @@ i=0
 while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
-  env $line timeout -k 10 180 python bench.py --steps $STEPS --warmup 5 --no-cpu-baseline ${ARGS:-} > $OUT/r$i.json 2> $OUT/r$i.err
+  env $line timeout -k 10 180 python bench.py --steps $STEPS --warmup ${WARM:-300} --no-cpu-baseline ${ARGS:-} > $OUT/r$i.json 2> $OUT/r$i.err
   rc=$?
   if [ $rc -ne 0 ]; then echo "[$line] rc=$rc"; tail -3 $OUT/r$i.err; exit $rc; fi
   python -c "
