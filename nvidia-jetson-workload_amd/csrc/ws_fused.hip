@@ -19,45 +19,12 @@
 #include <type_traits>
 #include <utility>
 
-#include "ws_fused.h"
+#include "ws_fused_dev.h"
 
 namespace ws {
 namespace {
 
-template <typename T>
-struct V3 {
-    T u, v, h;
-};
-
-// (a_r - a_l) / (2 d). POW2 (every 2dx, 2dy a power of two): the exact reciprocal gives the
-// same correctly rounded quotient; otherwise the IEEE divide.
-template <bool POW2, typename T>
-__device__ __forceinline__ T cdiff(T ar, T al, T two_d, T inv) {
-    if constexpr (POW2) return (ar - al) * inv;
-    else return (ar - al) / two_d;
-}
-
-// SWE tendency (weather_simulation.cpp:521-537), same evaluation order.
-template <bool POW2, typename T>
-__device__ __forceinline__ V3<T> tend(const V3<T>& c, const V3<T>& l, const V3<T>& r, const V3<T>& t,
-                                      const V3<T>& b, const Spacing<T>& sp, T g, T f) {
-    const T u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
-    const T u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
-    const T v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
-    const T v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
-    const T h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
-    const T h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
-    V3<T> k;
-    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
-    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
-    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
-    return k;
-}
-
-template <typename T>
-__device__ __forceinline__ V3<T> axpy(const V3<T>& y, T c, const V3<T>& k) {
-    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
-}
+using namespace dev;
 
 // LDS image, column-major: column c (= lane + 1; columns 0 and kFusedCols + 1 are pads)
 // holds, for every published quantity q = 2 * stage + (row parity), the three fields at
@@ -139,29 +106,39 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
     const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
     const int row_hi = g.bot_clamp ? g.H : g.H + NST;
 
+    // buffer addressing as in ws_fused_dpp.hip: per-field descriptors based at this
+    // workgroup's first row, row = scalar offset, column = fixed voffset; stores of
+    // non-output lanes / rows go to an out-of-range voffset and are dropped (no branch)
     const int64_t lofs = (int64_t)blockIdx.z * g.lstride;
-    const T* __restrict__ iu = a.in_u + lofs;
-    const T* __restrict__ iv = a.in_v + lofs;
-    const T* __restrict__ ih = a.in_h + lofs;
-    T* __restrict__ ou = a.out_u + lofs;
-    T* __restrict__ ov = a.out_v + lofs;
-    T* __restrict__ oh = a.out_h + lofs;
+    const int R0 = (y0 - NST) & ~1;  // march rows [R0, R1): R0 even (LDS parity), length a multiple of kU
+    const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;
+    const int rbase = max(R0, row_lo);
+    const int rtop = min(row_hi, R1 + kPf);
+    const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
+    const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
+    const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
+    const auto ru = make_rsrc(a.in_u + ib, in_bytes), rv = make_rsrc(a.in_v + ib, in_bytes),
+               rh = make_rsrc(a.in_h + ib, in_bytes);
+    const auto wu = make_rsrc(a.out_u + ob, out_bytes), wv = make_rsrc(a.out_v + ob, out_bytes),
+               wh = make_rsrc(a.out_h + ob, out_bytes);
+    const uint32_t row_bytes = (uint32_t)g.pitch * sizeof(T);
+    const uint32_t loff = (uint32_t)min(max(x, 0), g.W - 1) * sizeof(T);
+    const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : kDropped;
 
-    // Always-issued loads at clamped (allocated) addresses: dead rows / columns hold real
-    // data that no live output reads, and no branch splits the load stream.
-    const int xc = min(max(x, 0), g.W - 1);
+    // Always-issued loads at clamped (allocated) rows: dead rows / columns hold real data
+    // that no live output reads, and no branch splits the load stream.
     auto load_row = [&](int R) -> V3<T> {
         const int r = min(max(R, row_lo), row_hi - 1);
-        const int64_t i = (int64_t)r * g.pitch + xc;
-        return V3<T>{iu[i], iv[i], ih[i]};
+        const uint32_t so = (uint32_t)(r - rbase) * row_bytes;
+        return V3<T>{buf_load<T>(ru, loff, so), buf_load<T>(rv, loff, so), buf_load<T>(rh, loff, so)};
     };
     auto store_row = [&](int j, const V3<T>& o) {
-        if (xout && j >= y0 && j < y1) {
-            const int64_t i = (int64_t)j * g.pitch + x;
-            __builtin_nontemporal_store(o.u, ou + i);
-            __builtin_nontemporal_store(o.v, ov + i);
-            __builtin_nontemporal_store(o.h, oh + i);
-        }
+        const bool row_ok = j >= y0 && j < y1;
+        const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
+        const uint32_t vo = row_ok ? soff : kDropped;
+        buf_store_nt<T>(o.u, wu, vo, so);
+        buf_store_nt<T>(o.v, wv, vo, so);
+        buf_store_nt<T>(o.h, wh, vo, so);
     };
 
     V3<T> Y[kU];                // Y[r % kU] = y row r (rows R-kYb+1 .. R+kPf live)
@@ -173,16 +150,25 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
 #pragma unroll
     for (int i = 0; i < 2; ++i) S1[i] = S2[i] = S3[i] = K2[i] = K3[i] = Z;
 
-    // march rows [R0, R1): R0 even (one dead warm-up row if needed), length a multiple of kU
-    const int R0 = (y0 - NST) & ~1;
-    const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;
+    // prologue: each row followed by a (dropped) store row like every march body, so the
+    // loop is entered with the same outstanding-op pattern from here as from its back edge
 #pragma unroll
-    for (int i = 0; i < kPf; ++i) Y[i] = load_row(R0 + i);
+    for (int i = 0; i < kPf; ++i) {
+        Y[i] = load_row(R0 + i);
+        store_row(y0 - 1, Z);
+    }
 
-    auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
+    // Warm-up (the first kU bodies, Wc = true) skips stage s while R - R0 < 2s (outside the
+    // segment's dependency cone; R0 may sit one row above y0 - NST, which only makes the
+    // test conservative). Skipped stages publish nothing: the next stage to read that LDS
+    // quantity is itself inactive until a body after the first active one. A skipped final
+    // stage still issues its (dropped) store row: one load/store pattern for every body.
+    auto body = [&](auto Pc, auto Xc, auto Yc, auto Wc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
         constexpr bool YC = decltype(Yc)::value;
+        constexpr bool WARM = decltype(Wc)::value;
+        constexpr auto on = [](int st) { return !WARM || P >= 2 * st; };
         constexpr int cur = P & 1, prv = cur ^ 1;  // R0 even => parity of R is parity of P
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
@@ -197,58 +183,81 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
         using Q3c = std::integral_constant<int, 6 + cur>;
 
         Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+#if WS_SCHED_BARRIER
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads at the head of the body
+#endif
         pub(Q0c{}, Y[yi(0)]);
 
-        // stage 1 at row R-1 from y rows R-2, R-1, R
-        const V3<T> k1 = stage_tend<POW2, YC, NST, 0 + prv>(lcol, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1,
-                                                            a.gravity, a.coriolis_f);
-        if constexpr (NST == 1) {
-            store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
-        } else {
-            const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
-            // stage 2 at row R-2 from s1 rows R-3, R-2, R-1
-            const V3<T> k2 = stage_tend<POW2, YC, NST, 2 + prv>(lcol, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
-                                                                a.gravity, a.coriolis_f);
-            pub(Q1c{}, s1);
-            S1[r2(-1)] = s1;
-            if constexpr (NST == 2) {
-                store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+        if constexpr (on(1)) {
+            // stage 1 at row R-1 from y rows R-2, R-1, R
+            const V3<T> k1 = stage_tend<POW2, YC, NST, 0 + prv>(lcol, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)],
+                                                                a.sp1, a.gravity, a.coriolis_f);
+            if constexpr (NST == 1) {
+                store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
             } else {
-                const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
-                // stage 3 at row R-3
-                const V3<T> k3 = stage_tend<POW2, YC, NST, 4 + prv>(lcol, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2,
-                                                                    a.sp2, a.gravity, a.coriolis_f);
-                const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
-                // stage 4 at row R-4
-                const V3<T> k4 = stage_tend<POW2, YC, NST, 6 + prv>(lcol, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3,
-                                                                    a.sp2, a.gravity, a.coriolis_f);
-                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
-                const T two = T(2);
-                const V3<T>& y4 = Y[yi(-4)];
-                const V3<T>& kk2 = K2[r2(-4)];
-                const V3<T>& kk3 = K3[r2(-4)];
-                V3<T> o;
-                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
-                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
-                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
-                store_row(R - 4, o);
-                pub(Q2c{}, s2);
-                pub(Q3c{}, s3);
-                S2[r2(-2)] = s2;
-                S3[r2(-3)] = s3;
-                K2[r2(-2)] = k2;
-                K3[r2(-3)] = k3;
+                const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+                if constexpr (on(2)) {
+                    // stage 2 at row R-2 from s1 rows R-3, R-2, R-1
+                    const V3<T> k2 = stage_tend<POW2, YC, NST, 2 + prv>(lcol, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1,
+                                                                        a.sp2, a.gravity, a.coriolis_f);
+                    if constexpr (NST == 2) {
+                        store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+                    } else {
+                        const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                        if constexpr (on(3)) {
+                            // stage 3 at row R-3
+                            const V3<T> k3 = stage_tend<POW2, YC, NST, 4 + prv>(lcol, R - 3, g, S2[r2(-4)],
+                                                                                S2[r2(-3)], s2, a.sp2, a.gravity,
+                                                                                a.coriolis_f);
+                            const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
+                            if constexpr (on(4)) {
+                                // stage 4 at row R-4
+                                const V3<T> k4 = stage_tend<POW2, YC, NST, 6 + prv>(lcol, R - 4, g, S3[r2(-5)],
+                                                                                    S3[r2(-4)], s3, a.sp2,
+                                                                                    a.gravity, a.coriolis_f);
+                                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                                const T two = T(2);
+                                const V3<T>& y4 = Y[yi(-4)];
+                                const V3<T>& kk2 = K2[r2(-4)];
+                                const V3<T>& kk3 = K3[r2(-4)];
+                                V3<T> o;
+                                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
+                                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
+                                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                                store_row(R - 4, o);
+                            } else {
+                                store_row(y0 - 1, Z);
+                            }
+                            pub(Q3c{}, s3);
+                            S3[r2(-3)] = s3;
+                            K3[r2(-3)] = k3;
+                        } else {
+                            store_row(y0 - 1, Z);
+                        }
+                        pub(Q2c{}, s2);
+                        S2[r2(-2)] = s2;
+                        K2[r2(-2)] = k2;
+                    }
+                } else {
+                    store_row(y0 - 1, Z);
+                }
+                pub(Q1c{}, s1);
+                S1[r2(-1)] = s1;
             }
+        } else {
+            store_row(y0 - 1, Z);
         }
         __syncthreads();
     };
 
     auto march = [&](auto Xc, auto Yc) {
-        for (int R = R0; R < R1; R += kU) {
+        auto period = [&](auto Wc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-                (body(std::integral_constant<int, Ps>{}, Xc, Yc, R + Ps), ...);
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, Wc, R + Ps), ...);
             }(std::make_integer_sequence<int, kU>{});
-        }
+        };
+        period(std::true_type{}, R0);  // R1 - R0 >= kU: the march spans >= 2 NST rows
+        for (int R = R0 + kU; R < R1; R += kU) period(std::false_type{}, R);
     };
     // Global edges matter only to strips / segments within NST cells of them; every other
     // workgroup runs the clamp-free body.
@@ -270,6 +279,10 @@ hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, 
     if (g.W < 2) return hipErrorInvalidValue;  // x = 0 == W-1 needs two clamp copies: use the stage kernels
     const int out_w = kFusedCols - 2 * nstages;
     if (a.seg_n <= 0) return hipSuccess;
+    // buffer descriptors span one segment's rows (+ margins); 32-bit offsets, dropped-store
+    // voffset 2^31
+    if ((int64_t)(a.seg_rows + 2 * nstages + 2 * kU + kPf + 2) * g.pitch * (int64_t)sizeof(T) >= 0x7fffffff)
+        return hipErrorInvalidValue;
     const dim3 grid((g.W + out_w - 1) / out_w, a.seg_n, g.L);
     const dim3 block(kFusedCols);
     const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;

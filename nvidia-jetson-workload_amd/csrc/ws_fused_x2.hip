@@ -190,10 +190,15 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
     const int R0 = y0 - NST;
     const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
 
-    auto body = [&](auto Pc, auto Xc, auto Yc, int R) {
+    // Warm-up (the first kU bodies, Wc = true) skips stage s while R - R0 < 2s: those rows
+    // lie outside the segment's dependency cone (see ws_fused_dpp.hip). A skipped final
+    // stage still issues its (dropped) store row: every body keeps one load/store pattern.
+    auto body = [&](auto Pc, auto Xc, auto Yc, auto Wc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
         constexpr bool YC = decltype(Yc)::value;
+        constexpr bool WARM = decltype(Wc)::value;
+        constexpr auto on = [](int st) { return !WARM || P >= 2 * st; };
         constexpr auto yi = [](int d) { return ((P + d) % kNY + kNY) % kNY; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         Y[yi(kPf)] = load_row(Xc, R + kPf);  // its slot held row R + kPf - kNY: dead
@@ -208,47 +213,67 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
             return;
         }
 #endif
+        // RK4 with LDS rings: y row R-2 leaves the VGPR ring after this body (it is the s3
+        // base at R+1 and the output base at R+2); its LDS slot is row R-4's, so it is
+        // written after the final combination read that (a wave's LDS ops run in order)
+        auto put_y = [&] {
+            if constexpr (kLds) lds_put(kSlotY + r2(-2), Y[yi(-2)]);
+        };
+        if constexpr (!on(1)) {
+            store_row(Xc, y0 - 1, Z);
+            if constexpr (NST == 4) put_y();
+            return;
+        }
         const V3<VT> k1 = stage_tend<POW2, XC, YC>(e, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1, a.gravity,
                                                    a.coriolis_f);
         if constexpr (NST == 1) {
             store_row(Xc, R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
         } else {
             const V3<VT> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
-            const V3<VT> k2 = stage_tend<POW2, XC, YC>(e, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2, a.gravity,
-                                                       a.coriolis_f);
-            S1[r2(-1)] = s1;
-            if constexpr (NST == 2) {
-                store_row(Xc, R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
-            } else {
-                const V3<VT> s2 = axpy(Y[yi(-2)], a.c_half, k2);
-                const V3<VT> k3 = stage_tend<POW2, XC, YC>(e, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
+            if constexpr (on(2)) {
+                const V3<VT> k2 = stage_tend<POW2, XC, YC>(e, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
                                                            a.gravity, a.coriolis_f);
-                const V3<VT> y3 = kLds ? lds_get(kSlotY + r2(-3)) : Y[yi(-3)];
-                const V3<VT> s3 = axpy(y3, a.c_dt, k3);
-                const V3<VT> k4 = stage_tend<POW2, XC, YC>(e, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3, a.sp2,
-                                                           a.gravity, a.coriolis_f);
-                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
-                const T two = T(2);
-                const V3<VT> y4 = kLds ? lds_get(kSlotY + r2(-4)) : Y[yi(-4)];
-                const V3<VT> kk2 = kLds ? lds_get(kSlotK2 + r2(-4)) : K2[r2(-4)];
-                const V3<VT> kk3 = kLds ? lds_get(kSlotK3) : K3;
-                V3<VT> o;
-                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
-                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
-                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
-                store_row(Xc, R - 4, o);
-                S2[r2(-2)] = s2;
-                S3[r2(-3)] = s3;
-                if constexpr (kLds) {
-                    // slots of rows R-2 == those of R-4, read above (a wave's LDS ops run in order)
-                    lds_put(kSlotY + r2(-2), Y[yi(-2)]);  // leaves the VGPR ring next row
-                    lds_put(kSlotK2 + r2(-2), k2);
-                    lds_put(kSlotK3, k3);
+                if constexpr (NST == 2) {
+                    store_row(Xc, R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
                 } else {
-                    K2[r2(-2)] = k2;
-                    K3 = k3;
+                    const V3<VT> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                    if constexpr (on(3)) {
+                        const V3<VT> k3 = stage_tend<POW2, XC, YC>(e, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
+                                                                   a.gravity, a.coriolis_f);
+                        const V3<VT> y3 = kLds ? lds_get(kSlotY + r2(-3)) : Y[yi(-3)];
+                        const V3<VT> s3 = axpy(y3, a.c_dt, k3);
+                        if constexpr (on(4)) {
+                            const V3<VT> k4 = stage_tend<POW2, XC, YC>(e, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3,
+                                                                       a.sp2, a.gravity, a.coriolis_f);
+                            // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                            const T two = T(2);
+                            const V3<VT> y4 = kLds ? lds_get(kSlotY + r2(-4)) : Y[yi(-4)];
+                            const V3<VT> kk2 = kLds ? lds_get(kSlotK2 + r2(-4)) : K2[r2(-4)];
+                            const V3<VT> kk3 = kLds ? lds_get(kSlotK3) : K3;
+                            V3<VT> o;
+                            o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
+                            o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
+                            o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                            store_row(Xc, R - 4, o);
+                        } else {
+                            store_row(Xc, y0 - 1, Z);
+                        }
+                        S3[r2(-3)] = s3;  // after k4 read S3[r2(-5)] (same slot)
+                        if constexpr (kLds) lds_put(kSlotK3, k3);
+                        else K3 = k3;
+                    } else {
+                        store_row(Xc, y0 - 1, Z);
+                    }
+                    S2[r2(-2)] = s2;  // after k3 read S2[r2(-4)] (same slot)
+                    if constexpr (kLds) lds_put(kSlotK2 + r2(-2), k2);  // after the final read K2[r2(-4)]
+                    else K2[r2(-2)] = k2;
+                    put_y();
                 }
+            } else {
+                store_row(Xc, y0 - 1, Z);
+                if constexpr (NST == 4) put_y();
             }
+            S1[r2(-1)] = s1;  // after k2 read S1[r2(-3)] (same slot)
         }
     };
 
@@ -261,11 +286,13 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
             Y[i] = load_row(Xc, R0 + i);
             store_row(Xc, y0 - 1, Z);
         }
-        for (int R = R0; R < R1; R += kU) {
+        auto period = [&](auto Wc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-                (body(std::integral_constant<int, Ps>{}, Xc, Yc, R + Ps), ...);
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, Wc, R + Ps), ...);
             }(std::make_integer_sequence<int, kU>{});
-        }
+        };
+        period(std::true_type{}, R0);  // R1 - R0 >= kU: the march spans >= 2 NST rows
+        for (int R = R0 + kU; R < R1; R += kU) period(std::false_type{}, R);
     };
     // global edges matter only to strips / segments within reach of them
     const bool xclamp = base < 0 || base + kCols > g.W;

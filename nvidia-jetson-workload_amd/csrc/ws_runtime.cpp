@@ -518,8 +518,15 @@ void autotune(ws_sim* s) {
     for (Cand& c : cands) first += time_cand(c, 1);  // warm-up (code load, clocks)
     const int reps = (int)std::clamp(10.0f * (float)cands.size() / std::max(first, 1e-3f), 2.0f, 8.0f);
     for (Cand& c : cands) c.ms = 1e30f;
-    for (int round = 0; round < 3; ++round)
-        for (Cand& c : cands) c.ms = std::min(c.ms, time_cand(c, reps));
+    // at least 3 rounds, and until ~150 ms of device time: the chip's clocks ramp up over
+    // tens of milliseconds of load, and only warm timings rank the candidates right
+    float spent = first;
+    for (int round = 0; round < 12 && (round < 3 || spent < 150.f); ++round)
+        for (Cand& c : cands) {
+            const float t = time_cand(c, reps);
+            c.ms = std::min(c.ms, t);
+            spent += t * reps;
+        }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     const Cand* best = &cands[0];
