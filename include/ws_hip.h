@@ -235,7 +235,8 @@ int ws_sim_comm_barrier(ws_sim_t* sim);
 /* When enabled, every stage kernel of ws_sim_run / ws_sim_step is bracketed by hipEvents
  * on the simulation's stream. kind = stage index within the step (0..3 for RK4). The
  * statistics reset when timing is (re-)enabled. bytes_per_launch is the algorithmic
- * HBM traffic of one launch (SURVEY §8(d) words x cells x element size). */
+ * HBM traffic of one launch (SURVEY §8(d) words x cells x element size).
+ * enable = 0: off; 1: on; n > 1: on, with events for n launches created up front. */
 int ws_sim_set_kernel_timing(ws_sim_t* sim, int32_t enable);
 int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, double* total_ms,
                          double* bytes_per_launch);

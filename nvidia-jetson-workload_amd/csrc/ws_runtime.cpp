@@ -1223,8 +1223,10 @@ int ws_sim_comm_allreduce_max(ws_sim_t* s, double value, double* out) {
 int ws_sim_set_kernel_timing(ws_sim_t* s, int32_t enable) {
     return guarded([&] {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
+        set_device(s->device);
         s->timer.enable(enable != 0);
         s->timer.reset();
+        if (enable > 1) s->timer.reserve((size_t)enable);
     });
 }
 

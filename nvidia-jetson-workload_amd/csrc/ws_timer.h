@@ -22,6 +22,15 @@ public:
         for (hipEvent_t e : pool_) (void)hipEventDestroy(e);
     }
     void enable(bool on) { on_ = on; }
+    // pre-create events for n timed launches (hipEventCreate inside a timed run would
+    // stall the host between launches)
+    void reserve(size_t n) {
+        while (pool_.size() < 2 * n) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            pool_.push_back(e);
+        }
+    }
     bool enabled() const { return on_; }
     void reset() {
         for (auto& s : stats_) s = Stat{};

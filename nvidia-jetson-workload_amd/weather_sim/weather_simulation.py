@@ -654,8 +654,9 @@ class WeatherSimulation:
         check(lib.ws_sim_last_run_stats(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
-    def set_kernel_timing(self, enable=True):
-        check(lib.ws_sim_set_kernel_timing(self._h, 1 if enable else 0))
+    def set_kernel_timing(self, enable=True, reserve=0):
+        """Per-launch device timing; `reserve` launches get their events created now."""
+        check(lib.ws_sim_set_kernel_timing(self._h, max(2, int(reserve)) if enable and reserve else int(bool(enable))))
 
     def kernel_timing(self):
         """{stage kind: (launches, total device ms, algorithmic bytes per launch)}"""
