@@ -18,13 +18,25 @@ struct FusedArgs {
     Spacing<T> sp1;               // stage 1: spacing of the current grid
     Spacing<T> sp2;               // later stages: spacing of the temp grid (= config)
     int32_t seg_rows;             // output rows per workgroup segment
-    // segments processed by this launch: local index i < seg_na -> seg_a + i,
-    // else seg_b + (i - seg_na); seg_n in total (slab interior / edge split)
-    int32_t seg_a, seg_na, seg_b, seg_n;
+    // Output rows of this launch: two row groups, each cut into segments of seg_rows rows
+    // (the last one clipped): group A = [ga_y0, ga_y1) (ga_n segments), then group B =
+    // [gb_y0, gb_y1); seg_n segments in total. One group = the whole grid; a slab's
+    // interior launch uses A = the rows whose cone avoids the halo, its edge launch uses
+    // A, B = the few rows at the two slab boundaries.
+    int32_t ga_y0, ga_y1, ga_n;
+    int32_t gb_y0, gb_y1;
+    int32_t seg_n;
 };
 
-__host__ __device__ inline int fused_segment(int i, int seg_a, int seg_na, int seg_b) {
-    return i < seg_na ? seg_a + i : seg_b + (i - seg_na);
+template <typename T>
+__host__ __device__ inline void fused_rows(const FusedArgs<T>& a, int i, int& y0, int& y1) {
+    if (i < a.ga_n) {
+        y0 = a.ga_y0 + i * a.seg_rows;
+        y1 = y0 + a.seg_rows < a.ga_y1 ? y0 + a.seg_rows : a.ga_y1;
+    } else {
+        y0 = a.gb_y0 + (i - a.ga_n) * a.seg_rows;
+        y1 = y0 + a.seg_rows < a.gb_y1 ? y0 + a.seg_rows : a.gb_y1;
+    }
 }
 
 // nstages: 1 (Euler), 2 (RK2 midpoint), 4 (RK4-as-implemented)

@@ -101,10 +101,10 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
     T* const clampcol = lds.col(x == 0 ? lane : (x == g.W - 1 ? lane + 2 : (xlive ? lane + 1 : 0)));
     const T* const lcol = lds.col(lane);  // left neighbour column; right = lcol + 2 kCs
 
-    const int y0 = fused_segment(blockIdx.y, a.seg_a, a.seg_na, a.seg_b) * a.seg_rows;
-    const int y1 = min(y0 + a.seg_rows, g.H);
-    const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
-    const int row_hi = g.bot_clamp ? g.H : g.H + NST;
+    int y0, y1;
+    fused_rows(a, blockIdx.y, y0, y1);
+    const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
 
     // buffer addressing as in ws_fused_dpp.hip: per-field descriptors based at this
     // workgroup's first row, row = scalar offset, column = fixed voffset; stores of

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
-    const int seg = fused_segment((w / nstrips) % nsegs, a.seg_a, a.seg_na, a.seg_b);
+    int y0, y1;
+    fused_rows(a, (w / nstrips) % nsegs, y0, y1);
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
@@ -74,10 +75,8 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const bool xout = x >= 0 && x < g.W && lane >= NST && lane < kWave - NST;
     const bool xlo = x == 0, xhi = x == g.W - 1;
 
-    const int y0 = seg * a.seg_rows;
-    const int y1 = min(y0 + a.seg_rows, g.H);
-    const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
-    const int row_hi = g.bot_clamp ? g.H : g.H + NST;
+    const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
 
     // Buffer addressing: one descriptor per field, based at this wave's first row (all
     // wave-uniform, SGPRs), the row as a scalar byte offset, the lane's column as a fixed

@@ -95,7 +95,8 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
 
     const int w = xcd_work_item();
     const int strip = w % nstrips;
-    const int seg = fused_segment((w / nstrips) % nsegs, a.seg_a, a.seg_na, a.seg_b);
+    int y0, y1;
+    fused_rows(a, (w / nstrips) % nsegs, y0, y1);
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
@@ -107,10 +108,8 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
     e.hi0 = cx0 == g.W - 1;
     e.hi1 = cx0 + 1 == g.W - 1;
 
-    const int y0 = seg * a.seg_rows;
-    const int y1 = min(y0 + a.seg_rows, g.H);
-    const int row_lo = g.top_clamp ? 0 : -NST;  // rows that exist in memory (halo rows in slabs)
-    const int row_hi = g.bot_clamp ? g.H : g.H + NST;
+    const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
 
     // Buffer addressing (as ws_fused_dpp.hip): per-field descriptors based at this wave's
     // first row, the row as a scalar byte offset, the lane's column(s) as fixed voffsets;

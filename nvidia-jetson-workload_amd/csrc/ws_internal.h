@@ -9,9 +9,9 @@
 
 namespace ws {
 
-// Halo rows allocated above and below every field (slab exchange and the fused RK4
-// kernel's 4-row dependency cone).
-constexpr int kHalo = 4;
+// Halo rows allocated above and below every field: a slab exchanges up to 3 time steps'
+// worth of RK4 dependency cone (3 x 4 rows) at once (see ws_runtime.cpp, slab blocks).
+constexpr int kHalo = 12;
 
 enum StageMode : int {
     kAxpy = 0,       // out = base + c * k(in)                         (Euler, RK2, RK4 stage 1)
@@ -26,6 +26,7 @@ struct Geom {
     int64_t pitch;    // elements
     int64_t lstride;  // elements
     int32_t top_clamp, bot_clamp;  // 1: y-1 / y+1 clamp to self at row 0 / H-1 (global edge)
+    int32_t halo;                  // rows addressable above row 0 / below row H-1 (non-clamped sides)
 };
 
 template <typename T>

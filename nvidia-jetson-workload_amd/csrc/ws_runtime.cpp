@@ -107,6 +107,7 @@ struct ws_grid {
         ws::Geom g;
         g.W = W; g.H = H; g.L = L; g.pitch = pitch; g.lstride = lstride;
         g.top_clamp = top_clamp; g.bot_clamp = bot_clamp;
+        g.halo = ws::kHalo;
         return g;
     }
     size_t bytes_per_field() const { return (size_t)L * lstride * elem_size(dtype); }
@@ -228,8 +229,6 @@ struct ws_sim {
     int64_t last_launches = 0;
     ws::KernelTimer timer;
     int32_t rank = 0, nranks = 1;                       // y-slab position (1 = whole domain)
-    hipStream_t comm_stream = nullptr;                  // RCCL halo exchange (overlaps interior segments)
-    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
     bool own_stream = true;
     bool in_group = false;                              // a slab of a ws_group (local halo transport)
     bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
@@ -237,6 +236,8 @@ struct ws_sim {
     int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
     bool kernel_fixed = false, seg_fixed = false;
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
+    int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
+    int32_t block_pos = 0;    // position in the current block (0 = exchange first)
     int32_t want_blocks_override = 0;  // WS_WANT_BLOCKS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
@@ -310,28 +311,32 @@ int fused_stages(const ws_sim* s) {
 
 bool use_fused(const ws_sim* s) { return s->fused && s->slot[0]->W >= 2; }
 
-// Segments of a slab whose dependency cone (rows [y0 - nst, y1 + nst)) stays inside the
-// owned rows need no halo: they run while the halo exchange is in flight ("interior",
-// segments [k0, k1)); the others run after it ("edge").
-struct SegSplit {
-    int nsegs, k0, k1;
+// Output rows of a fused launch: [y0, y1) (empty if y1 <= y0).
+struct RowRange {
+    int y0, y1;
+    int rows() const { return y1 > y0 ? y1 - y0 : 0; }
 };
 
-SegSplit seg_split(const ws_sim* s, int nst) {
+// Slab blocks. A slab advances `block` steps per halo exchange: the exchange moves
+// block * NST rows of u, v, h from each neighbour, and step j = 0 .. block-1 of the block
+// computes its rows extended by (block - 1 - j) * NST into the halo on each non-global
+// side, so every step's dependency cone is covered by rows already on the device and the
+// last step of the block ends on exactly the owned rows. The extra work is
+// (block - 1) * NST * (block) rows per side per block; the saving is block - 1 exchanges and
+// every cross-stream synchronisation: the exchange is stream-ordered on the compute
+// stream (measured on MI355X: two cross-stream event waits per step cost more than an
+// overlapped edge launch saves).
+RowRange step_rows(const ws_sim* s, int nst) {
     const ws_grid* g = s->slot[0];
-    const int seg = s->seg_rows(nst);
-    SegSplit p;
-    p.nsegs = (g->H + seg - 1) / seg;
-    p.k0 = g->top_clamp ? 0 : (nst + seg - 1) / seg;
-    p.k1 = g->bot_clamp ? p.nsegs : std::max(0, (g->H - nst) / seg);
-    p.k0 = std::min(p.k0, p.nsegs);
-    p.k1 = std::max(p.k1, p.k0);
-    return p;
+    const int e = (s->block - 1 - s->block_pos) * nst;
+    return {g->top_clamp ? 0 : -e, g->bot_clamp ? g->H : g->H + e};
 }
 
-// Launch the fused step kernel over segments [segA, segA + nA) U [segB, segB + nB).
+// Launch the fused step kernel over the output rows A U B (segments of seg_rows rows).
 template <typename T>
-void fused_launch(ws_sim* s, int nst, int segA, int nA, int segB, int nB) {
+void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipStream_t st = nullptr) {
+    if (!st) st = s->stream;
+    const int nA = (A.rows() + seg_rows - 1) / seg_rows, nB = (B.rows() + seg_rows - 1) / seg_rows;
     if (nA + nB <= 0) return;
     ws_grid* c = s->slot[s->cur];
     ws_grid* n = s->slot[1 - s->cur];
@@ -346,16 +351,15 @@ void fused_launch(ws_sim* s, int nst, int segA, int nA, int segB, int nB) {
     a.coriolis_f = (T)s->cfg.coriolis_f;
     a.sp1 = make_spacing<T>(c->dx, c->dy);
     a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
-    a.seg_rows = s->seg_rows(nst);
-    a.seg_a = segA;
-    a.seg_na = nA;
-    a.seg_b = segB;
+    a.seg_rows = seg_rows;
+    a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
+    a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
     const ws::Geom g = c->geom();
     switch (s->kernel) {
-        case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, s->stream)); break;
-        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, s->stream)); break;
-        default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, s->stream)); break;
+        case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
+        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st)); break;
+        default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st)); break;
     }
     ++s->last_launches;
 }
@@ -374,19 +378,10 @@ void step_begin(ws_sim* s) {
     const ws::Geom g = c->geom();
     if (use_fused(s)) {
         const int nst = fused_stages(s);
-        const SegSplit p = seg_split(s, nst);
         s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L, s->stream);
-        if (s->nranks == 1) {
-            fused_launch<T>(s, nst, 0, p.nsegs, 0, 0);
-            return;
-        }
-        if (s->comm) {
-            WS_HIP_CHECK(hipEventRecord(s->ev_ready, s->stream));
-            WS_HIP_CHECK(hipStreamWaitEvent(s->comm_stream, s->ev_ready, 0));
-            s->comm->exchange(c->f, 3, (int)sizeof(T), g, nst, s->comm_stream);
-            WS_HIP_CHECK(hipEventRecord(s->ev_halo, s->comm_stream));
-        }
-        fused_launch<T>(s, nst, p.k0, p.k1 - p.k0, 0, 0);
+        // slab: at a block start, the block's halo (group slabs: copied by group_step)
+        if (s->block_pos == 0 && s->comm) s->comm->exchange(c->f, 3, (int)sizeof(T), g, s->block * nst, s->stream);
+        fused_launch<T>(s, nst, step_rows(s, nst), {0, 0}, s->seg_rows(nst));
         return;
     }
     if (method == WS_EULER) {
@@ -417,13 +412,8 @@ void step_end(ws_sim* s) {
     ws_grid* n = s->slot[1 - s->cur];
     const T dt = (T)s->dt;
     if (use_fused(s)) {
-        if (s->nranks > 1) {
-            const int nst = fused_stages(s);
-            const SegSplit p = seg_split(s, nst);
-            if (s->comm) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_halo, 0));
-            fused_launch<T>(s, nst, 0, p.k0, p.k1, p.nsegs - p.k1);
-        }
         s->timer.end(s->stream);
+        s->block_pos = (s->block_pos + 1) % s->block;
     }
     if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
         // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
@@ -474,7 +464,7 @@ int plan_steps(const ws_sim* s, int n) {
 template <typename T>
 void autotune(ws_sim* s) {
     s->tuned = true;
-    if (!use_fused(s) || s->kernel_fixed || s->in_group) return;
+    if (!use_fused(s) || s->kernel_fixed) return;
     const int nst = fused_stages(s);
     struct Cand {
         int kernel, seg;
@@ -505,9 +495,9 @@ void autotune(ws_sim* s) {
     auto time_cand = [&](Cand& c, int reps) {
         s->kernel = c.kernel;
         s->seg_override = c.seg;
-        const int nsegs = seg_split(s, nst).nsegs;
+        const int H = s->slot[0]->H, seg = s->seg_rows(nst);
         WS_HIP_CHECK(hipEventRecord(e0, s->stream));
-        for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, 0, nsegs, 0, 0);
+        for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, {0, H}, {0, 0}, seg);
         WS_HIP_CHECK(hipEventRecord(e1, s->stream));
         WS_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0.f;
@@ -545,6 +535,7 @@ void run_steps(ws_sim* s, int k) {
         else autotune<float>(s);
     }
     s->last_launches = 0;
+    s->block_pos = 0;  // every run starts a block: the halo is refreshed first
     WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
     for (int i = 0; i < k; ++i) {
         if (s->dtype == WS_F64) enqueue_step<double>(s);
@@ -574,10 +565,9 @@ void run_steps(ws_sim* s, int k) {
 void sim_free(ws_sim* s) {
     for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
         if (g) { grid_free(g); delete g; }
-    for (hipEvent_t e : {s->ev0, s->ev1, s->ev_ready, s->ev_halo})
+    for (hipEvent_t e : {s->ev0, s->ev1})
         if (e) (void)hipEventDestroy(e);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
-    if (s->comm_stream) (void)hipStreamDestroy(s->comm_stream);
     delete s->comm;
     delete s;
 }
@@ -615,15 +605,6 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         }
         WS_HIP_CHECK(hipEventCreate(&s->ev0));
         WS_HIP_CHECK(hipEventCreate(&s->ev1));
-        if (comm) {
-            // highest priority: the exchange's few workgroups must not queue behind the
-            // interior segments' thousands
-            int lo = 0, hi = 0;
-            WS_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            WS_HIP_CHECK(hipStreamCreateWithPriority(&s->comm_stream, hipStreamNonBlocking, hi));
-            WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
-            WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
-        }
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
@@ -637,7 +618,17 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             s->seg_fixed = s->seg_override > 0;
         }
         if (const char* e = std::getenv("WS_AUTOTUNE")) s->tuned = std::atoi(e) == 0;
+
         const int method = effective_method(*cfg);
+        if (slab.nranks > 1 && s->fused) {
+            // steps per exchange: as many as the halo (kHalo rows) and the thinnest slab
+            // (floor(H / nranks) rows, the same on every rank: neighbours must agree) allow,
+            // at most 3 (the extended-row overhead grows with the square of the block)
+            const int nst = method == WS_EULER ? 1 : method == WS_RK2 ? 2 : 4;
+            const int thin = cfg->grid_height / slab.nranks;
+            s->block = std::max(1, std::min(3, std::min(ws::kHalo, thin) / nst));
+            if (const char* e = std::getenv("WS_SLAB_BLOCK")) s->block = std::max(1, std::min(s->block, std::atoi(e)));
+        }
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
         if (!s->fused && method == WS_RK4) {
             s->tmpB = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
@@ -1126,7 +1117,7 @@ int ws_launch_shallow_water_kernel(const void* d_u, const void* d_v, const void*
         require(dx > 0 && dy > 0, WS_ERR_INVALID, "Grid spacing must be positive");
         ws::Geom g{};
         g.W = width; g.H = height; g.L = 1; g.pitch = pitch; g.lstride = pitch * height;
-        g.top_clamp = 1; g.bot_clamp = 1;
+        g.top_clamp = 1; g.bot_clamp = 1; g.halo = 0;
         auto body = [&](auto tag) {
             using T = decltype(tag);
             ws::StageArgs<T> a{};
@@ -1152,7 +1143,7 @@ int ws_launch_diagnostics_kernels(const void* d_u, const void* d_v, void* d_vort
         require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "bad dtype");
         ws::Geom g{};
         g.W = width; g.H = height; g.L = 1; g.pitch = pitch; g.lstride = pitch * height;
-        g.top_clamp = 1; g.bot_clamp = 1;
+        g.top_clamp = 1; g.bot_clamp = 1; g.halo = 0;
         if (dtype == WS_F64)
             WS_HIP_CHECK(ws::launch_diagnostics<double>((const double*)d_u, (const double*)d_v, (double*)d_vort,
                                                         (double*)d_div, make_spacing<double>(dx, dy), g,
@@ -1180,7 +1171,7 @@ int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, con
         require(cfg->grid_height >= nranks, WS_ERR_INVALID, "fewer rows than ranks");
         int r0 = 0, nrows = 0;
         ws::slab_rows(cfg->grid_height, rank, nranks, &r0, &nrows);
-        require(nranks == 1 || nrows >= ws::kHalo, WS_ERR_INVALID, "a slab needs at least 4 rows per rank");
+        require(nranks == 1 || nrows >= 4, WS_ERR_INVALID, "a slab needs at least 4 rows per rank");
         const int r1 = r0 + nrows;
         set_device(cfg->device_id);
         // a 1-rank slab still gets its communicator: same code path as N>1 (the exchanges
@@ -1301,9 +1292,12 @@ void group_exchange(ws_group* gr, int r, int depth) {
 
 template <typename T>
 void group_step(ws_group* gr) {
+    ws_sim* s0 = gr->slabs[0];
+    if (s0->block_pos == 0) {  // a block starts: the block's halo, by device copies
+        const int depth = s0->block * fused_stages(s0);
+        for (int r = 0; r < (int)gr->slabs.size(); ++r) group_exchange<T>(gr, r, depth);
+    }
     for (ws_sim* s : gr->slabs) step_begin<T>(s);
-    const int depth = fused_stages(gr->slabs[0]);
-    for (int r = 0; r < (int)gr->slabs.size(); ++r) group_exchange<T>(gr, r, depth);
     for (ws_sim* s : gr->slabs) step_end<T>(s);
 }
 
@@ -1314,7 +1308,7 @@ extern "C" {
 int ws_group_create(const ws_config_t* cfg, int32_t nslabs, ws_group_t** out) {
     return guarded([&] {
         require(cfg && out, WS_ERR_INVALID, "null pointer");
-        require(nslabs >= 1 && cfg->grid_height >= nslabs * ws::kHalo, WS_ERR_INVALID, "a slab needs >= 4 rows");
+        require(nslabs >= 1 && cfg->grid_height >= nslabs * 4, WS_ERR_INVALID, "a slab needs >= 4 rows");
         set_device(cfg->device_id);
         ws_group* gr = new ws_group;
         gr->device = cfg->device_id;
@@ -1367,6 +1361,16 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
         set_device(gr->device);
         const int k = plan_steps(gr->slabs[0], n);
         ws_sim* s0 = gr->slabs[0];
+        if (!s0->tuned && k > 0) {  // tune on slab 0, apply everywhere
+            if (s0->dtype == WS_F64) autotune<double>(s0);
+            else autotune<float>(s0);
+            for (ws_sim* s : gr->slabs) {
+                s->kernel = s0->kernel;
+                s->seg_override = s0->seg_override;
+                s->tuned = true;
+            }
+        }
+        for (ws_sim* s : gr->slabs) s->block_pos = 0;
         WS_HIP_CHECK(hipEventRecord(s0->ev0, gr->stream));
         for (int i = 0; i < k; ++i) {
             if (s0->dtype == WS_F64) group_step<double>(gr);

@@ -4,14 +4,16 @@ libws_hip.so's y-slab decomposition rests on three claims that d
 a GPU to check:
   1. ws_slab_partition's balanced rows cover the grid (rank r owns [row0, row0 + rows));
   2. a step of an n-stage integrator needs exactly n halo rows from each neighbour (the
-     fused kernel's dependency cone), clamped only at the global top/bottom edges, and the
-     end-of-run vorticity/divergence needs one fresh row of u, v;
+     fused kernel's dependency cone), so `block` steps need block x n rows: a slab that
+     receives block x n rows advances `block` steps before the next exchange (clamped only
+     at the global top/bottom edges); the end-of-run vorticity/divergence needs one fresh
+     row of u, v;
   3. bench.py's bootstrap (rank 0's RCCL unique id broadcast over gloo) and its
      max-over-ranks job time.
-Here each rank holds its slab, swaps n halo rows with its neighbours over gloo send/recv
-(the RCCL exchange's message pattern: top rows to rank-1, bottom rows to rank+1), steps the
-CPU oracle on the halo-extended slab, keeps its own rows, and compares them bit-for-bit
-with the oracle run on the whole grid. The GPU side of the same decomposition is tested
+Here each rank holds its slab, swaps block x n halo rows with its neighbours over gloo
+send/recv (the RCCL exchange's message pattern: top rows to rank-1, bottom rows to rank+1),
+steps the CPU oracle `block` steps on the halo-extended slab, keeps its own rows, and
+compares them bit-for-bit with the oracle run on the whole grid. The GPU side of the same decomposition is tested
 in tests/test_gpu_parity.py::test_slab_group_* and tests/test_gpu_slab_rccl.py.
 """
 import os
@@ -76,7 +78,7 @@ def _swap_halo(arrs, depth, rank, world):
     return top, bot
 
 
-def _worker(rank, world, port, method, fp64, steps):
+def _worker(rank, world, port, method, fp64, steps, block):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -98,15 +100,17 @@ def _worker(rank, world, port, method, fp64, steps):
         prec = "f64" if fp64 else "f32"
         full = _initial(np.float64 if fp64 else np.float32)
         own = [a[row0:row0 + rows].copy() for a in full]
-        depth = NST[method]
-
-        # 2. per step: swap `depth` halo rows, step the extended slab, keep the owned rows
-        for _ in range(steps):
-            top, bot = _swap_halo(own, depth, rank, world)
+        # 2. per block: swap block x NST halo rows, step the extended slab `block` times,
+        # keep the owned rows
+        done = 0
+        while done < steps:
+            nb = min(block, steps - done)
+            top, bot = _swap_halo(own, nb * NST[method], rank, world)
             ext = [np.concatenate([t, a, b]) for t, a, b in zip(top, own, bot)]
-            out = _oracle_step(ext, method, prec)
+            out = _oracle_step(ext, method, prec, steps=nb)
             lo = top[0].shape[0]
             own = [o[lo:lo + rows] for o in out[:3]]
+            done += nb
         top, bot = _swap_halo(own[:2], 1, rank, world)  # end-of-run u, v refresh for diagnostics
         ext = [np.concatenate([t, a, b]) for t, a, b in zip(top, own[:2], bot)]
         ext.append(np.concatenate([np.zeros_like(top[0]), own[2], np.zeros_like(bot[0])]))
@@ -124,11 +128,11 @@ def _worker(rank, world, port, method, fp64, steps):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,block", [(2, 1), (3, 1), (2, 3), (3, 2)])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_slab_protocol_matches_single_domain(world, method, fp64):
-    mp.spawn(_worker, args=(world, _free_port(), method, fp64, 5), nprocs=world, join=True)
+def test_slab_protocol_matches_single_domain(world, block, method, fp64):
+    mp.spawn(_worker, args=(world, _free_port(), method, fp64, 5, block), nprocs=world, join=True)
 
 
 def test_halo_depth_is_necessary():
