@@ -209,7 +209,7 @@ def main():
     cells = conf["W"] * conf["H"] * conf["L"]
     value = cells * args.steps / elapsed
     stats = sim.kernel_timing()
-    variant, seg_rows = sim.fused_variant()
+    variant, seg_rows, out_cols = sim.fused_variant()
     dev_ms, launches = sim.last_run_stats()
     # dominant kernel = largest total device time
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
@@ -239,7 +239,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
-                     "seg_rows": seg_rows, "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n},
+                     "seg_rows": seg_rows, "strip_out_cols": out_cols, "bytes_per_launch": bpl,
+                     "mean_launch_ms": tot_ms / n},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
         # SURVEY §8(d) prices the path as stage-by-stage passes (Euler 6w, RK2 15w, RK4 45w per
         # cell): the rate that traffic would need at the measured launch time

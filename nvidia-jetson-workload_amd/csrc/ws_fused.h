@@ -17,6 +17,7 @@ struct FusedArgs {
     T gravity, coriolis_f;
     Spacing<T> sp1;               // stage 1: spacing of the current grid
     Spacing<T> sp2;               // later stages: spacing of the temp grid (= config)
+    int32_t out_w;                // output columns per strip (<= strip columns - 2 margins)
     int32_t seg_rows;             // output rows per workgroup segment
     // Output rows of this launch: two row groups, each cut into segments of seg_rows rows
     // (the last one clipped): group A = [ga_y0, ga_y1) (ga_n segments), then group B =
@@ -48,8 +49,20 @@ constexpr int kDppCols = 64;
 template <typename T>
 hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
+// Strip geometry, per variant: columns per strip and the left margin (the dependency cone;
+// the x2 variant rounds it up to whole column pairs). The output window of strip s is
+// [s * out_w, (s + 1) * out_w); out_w is at most columns - 2 * margin, and when `aligned`
+// it is rounded down to whole 128-byte lines so no two strips write parts of one line.
+enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2 };
+inline int fused_strip_cols(int variant) { return variant == kFusedX2 ? 128 : variant == kFusedDpp ? 64 : 256; }
+inline int fused_margin(int variant, int nstages) { return variant == kFusedX2 ? (nstages + 1) / 2 * 2 : nstages; }
+inline int fused_out_w(int variant, int nstages, int elem_bytes, bool aligned) {
+    const int w = fused_strip_cols(variant) - 2 * fused_margin(variant, nstages);
+    const int line = 128 / elem_bytes;
+    return aligned && w >= line ? w / line * line : w;
+}
+
 // x2 variant: independent 64-lane waves, two adjacent columns per lane (128-column strips).
-int fused_x2_out_cols(int nstages);
 template <typename T>
 hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 

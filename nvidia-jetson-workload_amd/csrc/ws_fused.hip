@@ -93,10 +93,10 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
     __shared__ Lds<T, NST> lds;
 
     const int lane = threadIdx.x;
-    const int out_w = kFusedCols - 2 * NST;
+    const int out_w = a.out_w;
     const int x = blockIdx.x * out_w - NST + lane;  // this lane's global column
     const bool xlive = x >= 0 && x < g.W;
-    const bool xout = xlive && lane >= NST && lane < kFusedCols - NST;
+    const bool xout = xlive && lane >= NST && lane < NST + out_w;
     T* const mycol = lds.col(xlive ? lane + 1 : 0);
     T* const clampcol = lds.col(x == 0 ? lane : (x == g.W - 1 ? lane + 2 : (xlive ? lane + 1 : 0)));
     const T* const lcol = lds.col(lane);  // left neighbour column; right = lcol + 2 kCs
@@ -277,7 +277,8 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
 template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
     if (g.W < 2) return hipErrorInvalidValue;  // x = 0 == W-1 needs two clamp copies: use the stage kernels
-    const int out_w = kFusedCols - 2 * nstages;
+    const int out_w = a.out_w;
+    if (out_w < 1 || out_w > kFusedCols - 2 * nstages) return hipErrorInvalidValue;
     if (a.seg_n <= 0) return hipSuccess;
     // buffer descriptors span one segment's rows (+ margins); 32-bit offsets, dropped-store
     // voffset 2^31

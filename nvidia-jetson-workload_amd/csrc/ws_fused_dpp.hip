@@ -70,9 +70,9 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
-    const int out_w = kWave - 2 * NST;
+    const int out_w = a.out_w;
     const int x = strip * out_w - NST + lane;  // this lane's global column
-    const bool xout = x >= 0 && x < g.W && lane >= NST && lane < kWave - NST;
+    const bool xout = x >= 0 && x < g.W && lane >= NST && lane < NST + out_w;
     const bool xlo = x == 0, xhi = x == g.W - 1;
 
     const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
@@ -243,7 +243,8 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 
 template <typename T>
 hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
-    const int out_w = kWave - 2 * nstages;
+    const int out_w = a.out_w;
+    if (out_w < 1 || out_w > kWave - 2 * nstages) return hipErrorInvalidValue;
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (nsegs <= 0) return hipSuccess;

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
     constexpr int kU = unroll(NST);
     constexpr bool kLds = NST == 4 && WS_X2_LDS;
     constexpr int kM = margin(NST);
-    constexpr int kOutW = kCols - 2 * kM;
+    const int out_w = a.out_w;  // even: the window starts on a pair
 
     const int w = xcd_work_item();
     const int strip = w % nstrips;
@@ -100,9 +100,9 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
-    const int base = strip * kOutW - kM;  // global column of the strip's first column (even)
+    const int base = strip * out_w - kM;  // global column of the strip's first column (even)
     const int cx0 = base + 2 * lane;      // this lane's columns: cx0, cx0 + 1
-    const bool pair_out = 2 * lane >= kM && 2 * lane < kCols - kM;
+    const bool pair_out = 2 * lane >= kM && 2 * lane < kM + out_w;
     EdgeCols e;
     e.lo0 = cx0 == 0;
     e.hi0 = cx0 == g.W - 1;
@@ -307,11 +307,10 @@ __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T
 
 }  // namespace
 
-int fused_x2_out_cols(int nstages) { return kCols - 2 * margin(nstages); }
-
 template <typename T>
 hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
-    const int out_w = fused_x2_out_cols(nstages);
+    const int out_w = a.out_w;
+    if (out_w < 2 || out_w % 2 || out_w > kCols - 2 * margin(nstages)) return hipErrorInvalidValue;
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (nsegs <= 0) return hipSuccess;

@@ -207,7 +207,7 @@ void convert(Dst* d, const Src* s, size_t n) {
 // ------------------------------------------------------------------------------------
 // simulation
 // ------------------------------------------------------------------------------------
-enum FusedKernel : int { kKernLds = 0, kKernDpp = 1, kKernX2 = 2 };
+enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDpp = ws::kFusedDpp, kKernX2 = ws::kFusedX2 };
 
 struct ws_sim {
     ws_config_t cfg{};
@@ -234,7 +234,8 @@ struct ws_sim {
     bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
     int kernel = kKernDpp;    // fused kernel variant (WS_KERNEL=x2|dpp|lds fixes it)
     int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
-    bool kernel_fixed = false, seg_fixed = false;
+    bool align = false;       // strip output windows on whole 128-byte lines (WS_ALIGN fixes it)
+    bool kernel_fixed = false, seg_fixed = false, align_fixed = false;
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
@@ -243,11 +244,8 @@ struct ws_sim {
     ws::SlabComm* comm = nullptr;
     int32_t row0 = 0;
 
-    int64_t strips(int nst) const {
-        const int out_w = kernel == kKernX2 ? ws::fused_x2_out_cols(nst)
-                          : (kernel == kKernDpp ? ws::kDppCols : ws::kFusedCols) - 2 * nst;
-        return (slot[0]->W + out_w - 1) / out_w;
-    }
+    int out_w(int nst) const { return ws::fused_out_w(kernel, nst, (int)elem_size(dtype), align); }
+    int64_t strips(int nst) const { return (slot[0]->W + out_w(nst) - 1) / out_w(nst); }
     // segment rows giving about want_blocks workgroups (at least min_rows rows; the march
     // length rows + 2 NST a multiple of the unroll)
     int32_t seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const {
@@ -351,6 +349,7 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     a.coriolis_f = (T)s->cfg.coriolis_f;
     a.sp1 = make_spacing<T>(c->dx, c->dy);
     a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
+    a.out_w = s->out_w(nst);
     a.seg_rows = seg_rows;
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
@@ -468,25 +467,40 @@ void autotune(ws_sim* s) {
     const int nst = fused_stages(s);
     struct Cand {
         int kernel, seg;
+        bool align;
         float ms;
     };
     std::vector<Cand> cands;
+    const int fixed_seg = s->seg_override;
     for (int k : {kKernDpp, kKernX2, kKernLds}) {
-        s->kernel = k;
-        s->seg_override = 0;
-        if (s->seg_fixed) {
-            cands.push_back({k, s->seg_override, 0.f});
-            continue;
+        for (bool al : {false, true}) {
+            if (s->align_fixed && al != s->align) continue;
+            s->kernel = k;
+            const bool same = ws::fused_out_w(k, nst, (int)elem_size(s->dtype), true) ==
+                              ws::fused_out_w(k, nst, (int)elem_size(s->dtype), false);
+            if (al && same) continue;  // already aligned
+            // aligned windows below 3/4 of the strip waste too much recomputation
+            if (al && 4 * ws::fused_out_w(k, nst, (int)elem_size(s->dtype), true) < 3 * ws::fused_strip_cols(k))
+                continue;
+            const bool save_al = s->align;
+            s->align = al;
+            if (s->seg_fixed) {
+                cands.push_back({k, fixed_seg, al, 0.f});
+            } else {
+                // the default, and segment lengths giving whole multiples of the chip's wave
+                // slots (1024 SIMDs; an LDS workgroup is 4 waves) so no SIMD runs a lone
+                // extra wave
+                s->seg_override = 0;
+                std::vector<int> segs{s->seg_rows(nst)};
+                const int wave_per_block = k == kKernLds ? 4 : 1;
+                for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
+                    segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
+                std::sort(segs.begin(), segs.end());
+                segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
+                for (int seg : segs) cands.push_back({k, seg, al, 0.f});
+            }
+            s->align = save_al;
         }
-        // the default, and segment lengths giving whole multiples of the chip's wave slots
-        // (1024 SIMDs; an LDS workgroup is 4 waves) so no SIMD runs a lone extra wave
-        std::vector<int> segs{s->seg_rows(nst)};
-        const int wave_per_block = k == kKernLds ? 4 : 1;
-        for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
-            segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
-        std::sort(segs.begin(), segs.end());
-        segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
-        for (int seg : segs) cands.push_back({k, seg, 0.f});
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     WS_HIP_CHECK(hipEventCreate(&e0));
@@ -495,6 +509,7 @@ void autotune(ws_sim* s) {
     auto time_cand = [&](Cand& c, int reps) {
         s->kernel = c.kernel;
         s->seg_override = c.seg;
+        s->align = c.align;
         const int H = s->slot[0]->H, seg = s->seg_rows(nst);
         WS_HIP_CHECK(hipEventRecord(e0, s->stream));
         for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, {0, H}, {0, 0}, seg);
@@ -524,6 +539,7 @@ void autotune(ws_sim* s) {
         if (c.ms < best->ms) best = &c;
     s->kernel = best->kernel;
     s->seg_override = best->seg;
+    s->align = best->align;
     s->last_launches = 0;
 }
 
@@ -618,6 +634,10 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             s->seg_fixed = s->seg_override > 0;
         }
         if (const char* e = std::getenv("WS_AUTOTUNE")) s->tuned = std::atoi(e) == 0;
+        if (const char* e = std::getenv("WS_ALIGN")) {
+            s->align = std::atoi(e) != 0;
+            s->align_fixed = true;
+        }
 
         const int method = effective_method(*cfg);
         if (slab.nranks > 1 && s->fused) {
@@ -1232,12 +1252,13 @@ int ws_sim_kernel_timing(const ws_sim_t* s, int32_t kind, int64_t* launches, dou
     });
 }
 
-int ws_sim_fused_variant(const ws_sim_t* s, int32_t* kernel, int32_t* seg_rows) {
+int ws_sim_fused_variant(const ws_sim_t* s, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols) {
     return guarded([&] {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
         const bool fused = use_fused(s);
         if (kernel) *kernel = fused ? s->kernel : -1;
         if (seg_rows) *seg_rows = fused ? s->seg_rows(fused_stages(s)) : 0;
+        if (out_cols) *out_cols = fused ? s->out_w(fused_stages(s)) : 0;
     });
 }
 
@@ -1367,6 +1388,7 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
             for (ws_sim* s : gr->slabs) {
                 s->kernel = s0->kernel;
                 s->seg_override = s0->seg_override;
+                s->align = s0->align;
                 s->tuned = true;
             }
         }

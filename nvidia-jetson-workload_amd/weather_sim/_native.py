@@ -114,7 +114,7 @@ SIGNATURES = {
     "ws_group_run": [_P, _I, _PI],
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
-    "ws_sim_fused_variant": [_P, _PI, _PI],
+    "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
 }
 _RESTYPES = {"ws_last_error": ctypes.c_char_p, "ws_config_default": None}
 

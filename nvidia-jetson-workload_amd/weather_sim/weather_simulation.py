@@ -669,10 +669,12 @@ class WeatherSimulation:
         return out
 
     def fused_variant(self):
-        """(kernel name, rows per segment) of the fused step kernel in use (after the first run)."""
-        k, seg = ctypes.c_int32(), ctypes.c_int32()
-        check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg)))
-        return {-1: "stage_kernels", 0: "fused_lds", 1: "fused_dpp", 2: "fused_x2"}[k.value], seg.value
+        """(kernel name, rows per segment, output columns per strip) of the fused step kernel
+        in use (chosen at the first run)."""
+        k, seg, cols = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg), ctypes.byref(cols)))
+        return ({-1: "stage_kernels", 0: "fused_lds", 1: "fused_dpp", 2: "fused_x2"}[k.value], seg.value,
+                cols.value)
 
     def comm_allreduce_max(self, value):
         out = ctypes.c_double()

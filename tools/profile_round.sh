@@ -10,13 +10,17 @@ mkdir -p "$OUT/pmc"
 CFG=${CFG:-c2}; METHOD=${METHOD:-rk4}; STEPS=${STEPS:-50}; WARM=${WARM:-10}
 timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS --warmup $WARM > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
-read KERN KNAME SEG < <(python3 -c "
+read KERN KNAME SEG ALIGN < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
 k={'fused_dpp':'dpp','fused_dppdeep':'dppdeep','fused_x2':'x2','fused_lds':'lds'}.get(d['kernel'],'dpp')
 n={'dpp':'fused_dpp_kernel','dppdeep':'fused_dpp_kernel','x2':'fused_x2_kernel','lds':'fused_step_kernel'}[k]
-print(k, n, d.get('seg_rows') or 0)")
-echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG"
-export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG
+nst={'euler':1,'rk2':2,'rk4':4}['$METHOD']
+nst=2 if nst==4 and '$CFG' in ('c3','c4') else nst
+margin=(nst+1)//2*2 if k=='x2' else nst
+full={'dpp':64,'x2':128,'lds':256}[k]-2*margin
+print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0)")
+echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN"
+export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
