@@ -49,3 +49,15 @@ def test_x2_widths(W, method, fp64, monkeypatch):
 def test_x2_non_pow2(method, monkeypatch):
     monkeypatch.setenv("WS_KERNEL", "x2")
     run_both(301, 40, method, True, 4, dx=0.75, dy=1.3)
+
+
+@pytest.mark.parametrize("W", [61, 300, 700])
+@pytest.mark.parametrize("kernel", ["dpp", "x2", "lds"])
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_line_aligned_strips(W, kernel, method, fp64, monkeypatch):
+    """WS_ALIGN=1: strip output windows cut to whole 128-byte lines (asymmetric margins)."""
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_ALIGN", "1")
+    monkeypatch.setenv("WS_SEG_ROWS", "9")
+    run_both(W, 37, method, fp64, 5)
