@@ -175,7 +175,7 @@ class PerformanceMetrics:
 
 
 class OutputConfig:
-    """OutputConfig (output_manager.hpp:35-97); the file writers are out of scope."""
+    """OutputConfig (output_manager.hpp:35-47); the CSV writer is output.CSVOutputManager."""
 
     def __init__(self):
         self.output_dir = "./output"
@@ -184,7 +184,7 @@ class OutputConfig:
         self.output_interval = 10
         self.compress = False
         self.include_diagnostics = True
-        self.fields = ["velocity", "height", "vorticity"]
+        self.fields = ["velocity", "height", "pressure", "temperature", "humidity", "vorticity", "divergence"]
 
 
 class DeviceCapabilities:
@@ -574,16 +574,18 @@ class WeatherSimulation:
         t0 = time.perf_counter()
         if self._om is None:
             taken = self._run_native(num_steps)
-        else:  # output every output_interval steps needs the state between steps
+        else:  # writeOutput every output_interval steps (:84-88): run in chunks ending there
             taken = 0
             interval = self._config_py.output_interval
-            for _ in range(num_steps):
-                t_before = self.get_current_step()
-                self._run_native(1)
-                taken += 1
-                if interval > 0 and self.get_current_step() % interval == 0:
+            while taken < num_steps:
+                chunk = num_steps - taken
+                if interval > 0:
+                    chunk = min(chunk, interval - self.get_current_step() % interval)
+                k = self._run_native(chunk)
+                taken += k
+                if k > 0 and interval > 0 and self.get_current_step() % interval == 0:
                     self._om.write_output(self)
-                if self.get_current_step() == t_before or self.get_current_time() >= self._max_time():
+                if k < chunk or self.get_current_time() >= self._max_time():
                     break
         ms = (time.perf_counter() - t0) * 1000.0
         _say(f"Completed {num_steps} steps in {ms:.0f} ms ({ms / num_steps} ms/step)")
