@@ -118,6 +118,8 @@ int ws_abi_version(void);
 int ws_is_available(int32_t* available);
 int ws_device_count(int32_t* count);
 int ws_device_info(int32_t device, ws_device_info_t* out);
+/* hipMemGetInfo of a device (the benchmark harness's device-memory figure) */
+int ws_device_memory(int32_t device, int64_t* free_bytes, int64_t* total_bytes);
 void ws_config_default(ws_config_t* cfg);
 
 /* ---- WeatherGrid ---------------------------------------------------------------- */

@@ -725,6 +725,16 @@ int ws_device_info(int32_t device, ws_device_info_t* out) {
     });
 }
 
+int ws_device_memory(int32_t device, int64_t* free_bytes, int64_t* total_bytes) {
+    return guarded([&] {
+        set_device(device);
+        size_t fr = 0, tot = 0;
+        WS_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        if (free_bytes) *free_bytes = (int64_t)fr;
+        if (total_bytes) *total_bytes = (int64_t)tot;
+    });
+}
+
 void ws_config_default(ws_config_t* c) {
     if (!c) return;
     std::memset(c, 0, sizeof(*c));

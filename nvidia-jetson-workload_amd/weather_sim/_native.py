@@ -68,6 +68,7 @@ SIGNATURES = {
     "ws_is_available": [_PI],
     "ws_device_count": [_PI],
     "ws_device_info": [_I, ctypes.POINTER(ws_device_info_t)],
+    "ws_device_memory": [_I, _PL, _PL],
     "ws_config_default": [ctypes.POINTER(ws_config_t)],
     "ws_grid_create": [_I, _I, _I, _I, _I, _PP],
     "ws_grid_destroy": [_P],
