@@ -46,18 +46,31 @@ template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 // DPP variant: independent 64-lane waves, horizontal neighbours by DPP lane shifts.
 constexpr int kDppCols = 64;
+// dma: y rows staged through LDS by LDS-DMA (16 B per lane) instead of VGPR loads
 template <typename T>
-hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, bool dma);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone;
 // the x2 variant rounds it up to whole column pairs). The output window of strip s is
 // [s * out_w, (s + 1) * out_w); out_w is at most columns - 2 * margin, and when `aligned`
 // it is rounded down to whole 128-byte lines so no two strips write parts of one line.
-enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2 };
-inline int fused_strip_cols(int variant) { return variant == kFusedX2 ? 128 : variant == kFusedDpp ? 64 : 256; }
-inline int fused_margin(int variant, int nstages) { return variant == kFusedX2 ? (nstages + 1) / 2 * 2 : nstages; }
+enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3 };
+inline int fused_strip_cols(int variant) {
+    return variant == kFusedX2 ? 128 : (variant == kFusedDpp || variant == kFusedDppDma) ? 64 : 256;
+}
+// (the DMA variant rounds it up to whole 16-byte chunks: a strip's LDS-DMA chunks then
+// never straddle column 0, where a partly negative chunk would be dropped whole by the
+// buffer range check)
+inline int fused_margin(int variant, int nstages, int elem_bytes) {
+    if (variant == kFusedX2) return (nstages + 1) / 2 * 2;
+    if (variant == kFusedDppDma) {
+        const int g = 16 / elem_bytes;
+        return (nstages + g - 1) / g * g;
+    }
+    return nstages;
+}
 inline int fused_out_w(int variant, int nstages, int elem_bytes, bool aligned) {
-    const int w = fused_strip_cols(variant) - 2 * fused_margin(variant, nstages);
+    const int w = fused_strip_cols(variant) - 2 * fused_margin(variant, nstages, elem_bytes);
     const int line = 128 / elem_bytes;
     return aligned && w >= line ? w / line * line : w;
 }

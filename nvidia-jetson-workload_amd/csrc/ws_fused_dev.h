@@ -44,6 +44,15 @@ __device__ __forceinline__ void buf_store_nt(V v, __amdgpu_buffer_rsrc_t r, uint
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, kNT);
 }
 
+// LDS-DMA: 16 bytes per lane from the buffer into LDS at lds + 16 * lane (wave-uniform base;
+// buffer_load_dwordx4 ... lds). Completion is counted by vmcnt; the compiler does not order
+// later LDS reads after it, callers wait explicitly. (A device function, not a lambda: the
+// builtin inside a kernel-local lambda silently drops the kernel's host launch stub.)
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff) {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)lds, 16, (int)voff, 0, 0, 0);
+}
+
 // ---- DPP lane shifts -------------------------------------------------------------------
 // lane i <- lane i-1 (wave_shr:1) / lane i <- lane i+1 (wave_shl:1). Lanes without a source
 // read 0 (bound_ctrl): a strip's edge lanes, whose results lie in the discarded margin.

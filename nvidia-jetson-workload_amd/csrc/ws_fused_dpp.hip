@@ -25,7 +25,7 @@ constexpr int kWave = 64;
 // rows of y loads in flight per lane (template parameter PF; 3 measured best at C2 -- a
 // 6-row variant did not help even on grids too small to fill the chip)
 constexpr int unroll_for(int pf) { return (5 + pf + 1) / 2 * 2; }  // y ring length (>= 5 past rows + pf, even)
-constexpr int kUMax = unroll_for(WS_DPP_PF);
+constexpr int kUMax = unroll_for(WS_DPP_PF) > 16 ? unroll_for(WS_DPP_PF) : 16;
 
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
 // XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
@@ -55,13 +55,35 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
 #define WS_DPP_MINW 1
 #endif
 
+// s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
+// lgkmcnt[11:8], vmcnt[15:14]); the other counters at their maxima = not waited on
+constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// PF > 0: y rows loaded PF rows ahead into VGPRs (buffer_load, 8 or 4 bytes per lane).
+// PF == 0 ("DMA"): y rows staged through an LDS ring by LDS-DMA -- buffer_load_dwordx4 ...
+// lds, 16 bytes per lane, one instruction per field moves kG = 16 / sizeof(T) rows of the
+// strip -- kD rows ahead, with no VGPR held by a load in flight; each group of kG rows is
+// copied LDS -> VGPR ring one body before its first row is needed. The compiler does not
+// order LDS reads after LDS-DMA writes, so the kernel waits itself: every body issues
+// exactly 3 stores and every kG-th body 3 DMAs, hence a fixed count of younger vector-
+// memory ops at each wait (kWaitN below).
 template <typename T, int NST, bool POW2, int PF>
 __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
-    constexpr int kPf = PF;
-    constexpr int kU = unroll_for(PF);
+    constexpr bool kDma = PF == 0;
+    constexpr int kG = 16 / (int)sizeof(T);                    // rows per DMA instruction
+    constexpr int kNR = (int)sizeof(T) == 8 ? 8 : 16;          // LDS ring rows
+    constexpr int kD = kDma ? ((int)sizeof(T) == 8 ? 6 : 8) : 0;  // DMA rows in flight
+    constexpr int kPf = kDma ? 0 : PF;
+    constexpr int kU = kDma ? kNR : unroll_for(PF);            // DMA: ring slot == y ring index
     constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
-    static_assert(kYb + kPf <= kU, "y ring too short");
+    static_assert(kDma || kYb + kPf <= kU, "y ring too short");
+    // a group's DMA may overwrite only slots whose rows were consumed (compiler lgkmcnt wait) in
+    // an earlier body: kNR >= kD + kG
+    static_assert(!kDma || (kU % kG == 0 && kU > kG + 4 && kNR >= kD + kG && kD % kG == 0), "DMA ring");
+    // younger vector-memory ops than a group's DMAs when that group is read: the stores of
+    // the kD - 1 bodies from its issue on, and the DMAs issued in between
+    constexpr int kWaitN = 3 * (kD - 1) + 3 * ((kD - 1) / (kG > 0 ? kG : 1));
 
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
@@ -70,9 +92,11 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const int level = w / (nstrips * nsegs);
 
     const int lane = threadIdx.x;
+    // left margin: the cone (NST), for DMA rounded up to whole 16-byte chunks
+    constexpr int kM = kDma ? (NST + kG - 1) / kG * kG : NST;
     const int out_w = a.out_w;
-    const int x = strip * out_w - NST + lane;  // this lane's global column
-    const bool xout = x >= 0 && x < g.W && lane >= NST && lane < NST + out_w;
+    const int x = strip * out_w - kM + lane;  // this lane's global column
+    const bool xout = x >= 0 && x < g.W && lane >= kM && lane < kM + out_w;
     const bool xlo = x == 0, xhi = x == g.W - 1;
 
     const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
@@ -85,7 +109,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     // (no exec-mask branch). launch_fused_step_dpp checks the byte ranges fit.
     const int64_t lofs = (int64_t)level * g.lstride;
     const int rbase = max(y0 - NST, row_lo);
-    const int rtop = min(row_hi, y1 + NST + kU + kPf);  // past the last row the march loads
+    const int rtop = min(row_hi, y1 + NST + kU + (kDma ? kD + kG : kPf));  // past the last row the march loads
     const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
     const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
     const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
@@ -124,6 +148,25 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         buf_store_nt<T>(o.h, wh, vo, so);
     };
 
+    // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG
+    // consecutive slots (64 lanes x 16 B = kG rows of 64 columns)
+    __shared__ __attribute__((aligned(16))) T ring[kDma ? 3 : 1][kDma ? kNR : 1][kWave];
+    const int dk = lane / (kWave / kG);                          // row of the group this lane fetches
+    const int dcol = (strip * out_w - kM) * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // byte column (16-B aligned)
+    auto dma = [&](int q, int slot) {  // rows q .. q + kG - 1 into slots slot .. slot + kG - 1
+        const int r = min(max(q + dk, row_lo), row_hi - 1);
+        // chunks left of column 0 (whole chunks: kM is chunk-aligned) wrap to huge offsets or
+        // read the previous row, chunks past the row end read the next row: margin lanes
+        // only, never read by an output lane
+        const uint32_t vo = (uint32_t)((r - rbase) * (int)row_bytes + dcol);
+        lds_dma16(ru, &ring[0][slot][0], vo);
+        lds_dma16(rv, &ring[1 % (kDma ? 3 : 1)][slot][0], vo);
+        lds_dma16(rh, &ring[2 % (kDma ? 3 : 1)][slot][0], vo);
+    };
+    auto read_row = [&](int slot) -> V3<T> {
+        return V3<T>{ring[0][slot][lane], ring[1 % (kDma ? 3 : 1)][slot][lane], ring[2 % (kDma ? 3 : 1)][slot][lane]};
+    };
+
     const V3<T> Z{T(0), T(0), T(0)};
     V3<T> Y[kU];                 // Y[r % kU] = y row r
     V3<T> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
@@ -137,10 +180,27 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     const int R1 = R0 + (y1 + NST - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
     // prologue: each row followed by a (dropped) store row like every march body, so the
     // loop is entered with the same outstanding-op pattern from here as from its back edge
+    if constexpr (kDma) {
+        // the kD virtual bodies before R0: DMAs for rows R0 .. R0 + kD - 1, stores, and the
+        // copy of the first group into the y ring
+        [&]<int... Vs>(std::integer_sequence<int, Vs...>) {
+            ([&] {
+                constexpr int v = Vs - kD;  // -kD .. -1
+                if constexpr (((v % kG) + kG) % kG == 0) dma(R0 + v + kD, v + kD);
+                store_row(y0 - 1, Z);
+                if constexpr (v == -1) {
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
 #pragma unroll
-    for (int i = 0; i < kPf; ++i) {
-        Y[i] = load_row(R0 + i);
-        store_row(y0 - 1, Z);
+                    for (int k = 0; k < kG; ++k) Y[k] = read_row(k);
+                }
+            }(), ...);
+        }(std::make_integer_sequence<int, kD>{});
+    } else {
+#pragma unroll
+        for (int i = 0; i < kPf; ++i) {
+            Y[i] = load_row(R0 + i);
+            store_row(y0 - 1, Z);
+        }
     }
 
     // Warm-up (the first kU bodies of a segment, Wc = true): stage s at row R - s is needed
@@ -156,7 +216,16 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         constexpr auto on = [](int st) { return !WARM || P >= 2 * st; };
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
-        Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        if constexpr (kDma) {
+            if constexpr (P % kG == 0) dma(R + kD, (P + kD) % kNR);  // slots of rows R+kD-kNR..: read
+            if constexpr ((P + 1) % kG == 0) {  // rows R+1 .. R+kG: LDS -> y ring, needed from R+1 on
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
+#pragma unroll
+                for (int k = 1; k <= kG; ++k) Y[yi(k)] = read_row((P + k) % kNR);
+            }
+        } else {
+            Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
+        }
         // keep the row's loads at the head of the body: the scheduler would otherwise sink
         // them below the stencil math, shortening the prefetch distance
 #if WS_SCHED_BARRIER
@@ -226,6 +295,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         };
         period(std::true_type{}, R0);  // R1 - R0 >= kU: the march spans >= 2 NST rows
         for (int R = R0 + kU; R < R1; R += kU) period(std::false_type{}, R);
+        if constexpr (kDma) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     // global edges matter only to strips / segments within NST cells of them
     const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - NST;
@@ -242,9 +312,11 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 }  // namespace
 
 template <typename T>
-hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, bool dma) {
     const int out_w = a.out_w;
-    if (out_w < 1 || out_w > kWave - 2 * nstages) return hipErrorInvalidValue;
+    if (out_w < 1 || out_w > kWave - 2 * fused_margin(dma ? kFusedDppDma : kFusedDpp, nstages, (int)sizeof(T)))
+        return hipErrorInvalidValue;
+    if (dma && out_w % (16 / (int)sizeof(T)) != 0) return hipErrorInvalidValue;  // chunk-aligned strips
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (nsegs <= 0) return hipSuccess;
@@ -257,9 +329,14 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     const dim3 grid((unsigned)nblocks), block(kWave);
     const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
 #define WS_DPP_GO(N, P2, PF) hipLaunchKernelGGL((fused_dpp_kernel<T, N, P2, PF>), grid, block, 0, s, a, g, nstrips, nsegs)
-#define WS_DPP_LAUNCH(N)              \
-    if (pow2) WS_DPP_GO(N, true, WS_DPP_PF); \
-    else WS_DPP_GO(N, false, WS_DPP_PF);
+#define WS_DPP_LAUNCH(N)                     \
+    if (dma) {                                  \
+        if (pow2) WS_DPP_GO(N, true, 0);        \
+        else WS_DPP_GO(N, false, 0);            \
+    } else {                                    \
+        if (pow2) WS_DPP_GO(N, true, WS_DPP_PF); \
+        else WS_DPP_GO(N, false, WS_DPP_PF);    \
+    }
     switch (nstages) {
         case 1: WS_DPP_LAUNCH(1) break;
         case 2: WS_DPP_LAUNCH(2) break;
@@ -271,7 +348,7 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     return hipGetLastError();
 }
 
-template hipError_t launch_fused_step_dpp<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t);
-template hipError_t launch_fused_step_dpp<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t);
+template hipError_t launch_fused_step_dpp<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t, bool);
+template hipError_t launch_fused_step_dpp<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t, bool);
 
 }  // namespace ws

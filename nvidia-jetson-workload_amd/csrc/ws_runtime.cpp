@@ -207,7 +207,8 @@ void convert(Dst* d, const Src* s, size_t n) {
 // ------------------------------------------------------------------------------------
 // simulation
 // ------------------------------------------------------------------------------------
-enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDpp = ws::kFusedDpp, kKernX2 = ws::kFusedX2 };
+enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDpp = ws::kFusedDpp, kKernX2 = ws::kFusedX2,
+                         kKernDppDma = ws::kFusedDppDma };
 
 struct ws_sim {
     ws_config_t cfg{};
@@ -262,7 +263,7 @@ struct ws_sim {
     // warm-up rows stay a small overhead. The autotuner also tries other counts.
     int32_t seg_rows(int nst) const {
         if (seg_override > 0) return seg_override;
-        int64_t want_blocks = kernel == kKernX2 ? 2048 : kernel == kKernDpp ? 4096 : 512;
+        int64_t want_blocks = kernel == kKernX2 ? 2048 : (kernel == kKernDpp || kernel == kKernDppDma) ? 4096 : 512;
         if (want_blocks_override > 0) want_blocks = want_blocks_override;
         return seg_for_blocks(nst, want_blocks, 24 * nst);
     }
@@ -357,7 +358,8 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     const ws::Geom g = c->geom();
     switch (s->kernel) {
         case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
-        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st)); break;
+        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, false)); break;
+        case kKernDppDma: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, true)); break;
         default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st)); break;
     }
     ++s->last_launches;
@@ -472,7 +474,7 @@ void autotune(ws_sim* s) {
     };
     std::vector<Cand> cands;
     const int fixed_seg = s->seg_override;
-    for (int k : {kKernDpp, kKernX2, kKernLds}) {
+    for (int k : {kKernDpp, kKernDppDma, kKernX2, kKernLds}) {
         for (bool al : {false, true}) {
             if (s->align_fixed && al != s->align) continue;
             s->kernel = k;
@@ -625,7 +627,10 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
         if (const char* e = std::getenv("WS_KERNEL")) {
-            s->kernel = std::strcmp(e, "lds") == 0 ? kKernLds : std::strcmp(e, "dpp") == 0 ? kKernDpp : kKernX2;
+            s->kernel = std::strcmp(e, "lds") == 0      ? kKernLds
+                        : std::strcmp(e, "dpp") == 0    ? kKernDpp
+                        : std::strcmp(e, "dppdma") == 0 ? kKernDppDma
+                                                        : kKernX2;
             s->kernel_fixed = true;
         }
         if (const char* e = std::getenv("WS_WANT_BLOCKS")) s->want_blocks_override = std::atoi(e);
