@@ -554,6 +554,13 @@ void run_steps(ws_sim* s, int k) {
     }
     s->last_launches = 0;
     s->block_pos = 0;  // every run starts a block: the halo is refreshed first
+    // one fused launch per step and nothing else on the stream: the kernel's mean duration
+    // is the run's span / k (no timestamp packets between the launches being measured)
+    const bool span = s->timer.enabled() && use_fused(s) && !s->comm &&
+                      s->cfg.model != WS_MODEL_PRIMITIVE_EQUATIONS;
+    s->timer.suspend(span);
+    // otherwise (halo exchanges or PE T/P updates share the stream) time every 8th launch
+    s->timer.sample_period(span || !use_fused(s) ? 1 : 8);
     WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
     for (int i = 0; i < k; ++i) {
         if (s->dtype == WS_F64) enqueue_step<double>(s);
@@ -574,6 +581,11 @@ void run_steps(ws_sim* s, int k) {
     s->timer.collect();
     float ms = 0.f;
     WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    if (span) {
+        const ws::Geom g = s->slot[0]->geom();
+        s->timer.add_span(0, 6.0 * elem_size(s->dtype) * g.W * g.H * g.L, s->last_launches, ms);
+        s->timer.suspend(false);
+    }
     s->last_ms = ms;
     s->metrics.compute_time_ms += ms;
     s->metrics.total_time_ms += ms;

@@ -34,17 +34,19 @@ public:
     bool enabled() const { return on_; }
     void reset() {
         for (auto& s : stats_) s = Stat{};
+        for (auto& n : seen_) n = 0;
         used_ = 0;
         pending_.clear();
     }
     void begin(int kind, double bytes, hipStream_t s) {
-        if (!on_) return;
+        if (!on_ || suspended_) return;
+        if (period_ > 1 && (seen_[kind]++ % period_) != 0) return;  // sampled launches only
         hipEvent_t e = get();
         (void)hipEventRecord(e, s);
         pending_.push_back({kind, bytes, e, nullptr});
     }
     void end(hipStream_t s) {
-        if (!on_) return;
+        if (!on_ || suspended_ || pending_.empty() || pending_.back().e1) return;
         hipEvent_t e = get();
         (void)hipEventRecord(e, s);
         pending_.back().e1 = e;
@@ -63,6 +65,21 @@ public:
         pending_.clear();
         used_ = 0;
     }
+    // Whole-run attribution: `launches` back-to-back launches of one kernel were the only
+    // work on the stream between two events `ms` apart (per-launch events would put two
+    // timestamp packets between consecutive kernels of the run they measure).
+    void add_span(int kind, double bytes, int64_t launches, double ms) {
+        if (!on_ || launches <= 0) return;
+        Stat& st = stats_[kind];
+        st.launches += launches;
+        st.total_ms += ms;
+        st.bytes_per_launch = bytes;
+    }
+    // suspend per-launch events (begin/end become no-ops) while a span is measured
+    void suspend(bool off) { suspended_ = off; }
+    // time one launch in `p` per kind (every launch: 1); the mean over the sampled launches
+    // stands for all of them, and the other launches run without timestamp packets
+    void sample_period(int p) { period_ = p > 1 ? p : 1; }
     const Stat& stat(int kind) const { return stats_[kind]; }
 
 private:
@@ -80,6 +97,9 @@ private:
         return pool_[used_++];
     }
     bool on_ = false;
+    bool suspended_ = false;
+    int period_ = 1;
+    int64_t seen_[kKinds] = {};
     std::vector<hipEvent_t> pool_;
     size_t used_ = 0;
     std::vector<Pending> pending_;

@@ -10,7 +10,7 @@ STEPS=${STEPS:-20}
 WARM=${WARM:-5}
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 
-timeout -k 10 ${PYTEST_T:-400} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 ${PYTEST_T:-400} python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
 ok $rc || exit $rc
 
