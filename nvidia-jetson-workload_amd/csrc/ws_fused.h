@@ -27,7 +27,46 @@ struct FusedArgs {
     int32_t ga_y0, ga_y1, ga_n;
     int32_t gb_y0, gb_y1;
     int32_t seg_n;
+    // 1 = "scaled tendencies" (set by scale_tendencies, below): the kernels leave the
+    // central differences unscaled and every constant that multiplies them carries the
+    // 1/(2 dx) factor instead; 0 = the kernels divide by (2 dx) as the reference writes it
+    int32_t scaled;
 };
+
+// Scaled tendencies. When 2dx = 2dy = 2^-k for both spacings (s = 1/(2dx) = 2^k), every
+// tendency the reference computes is s times the same expression evaluated on the raw
+// differences D = (ar - al): multiplying by a power of two commutes with IEEE rounding, so
+//   (-u)*(s*D) = s*round((-u)*D),   g*(s*D) = s*round(g*D),   s*A - s*B = s*round(A - B),
+//   f*v = s*round((f/s)*v),   y + c*(s*K) = y + round((c*s)*K),   s*a + 2*(s*b) = s*round(a + 2*b),
+// with f/s and c*s exact. The kernels evaluate K = k/s (g unchanged, f -> f/s) and the
+// update constants carry s, skipping the 6 multiplications by s per stage (RK4: 24 of ~170
+// fp64 ops per cell). Results are bit-identical to the reference's
+// evaluation order whenever no intermediate is subnormal (|x| < 2^-1022 fp64, 2^-126 fp32)
+// or within a factor 2^|k| of overflow. Subnormal intermediates do occur (the reference
+// fixture "mountain" fp32 after 50 steps: values ~1e-42 ahead of the wave front differ in
+// their last subnormal bits), so this is OPT-IN (WS_SCALED=1): the default is bit-exact.
+// Spacing modes of the fused kernels (template parameter): divide as the reference writes
+// it; multiply by the exact reciprocal (2dx, 2dy powers of two: bit-identical); scaled.
+enum SpacingMode : int { kSpDiv = 0, kSpMul = 1, kSpScaled = 2 };
+template <typename T>
+inline int fused_sp_mode(const FusedArgs<T>& a) {
+    if (a.scaled) return kSpScaled;
+    return a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y ? kSpMul : kSpDiv;
+}
+
+template <typename T>
+inline void scale_tendencies(FusedArgs<T>& a) {
+    const Spacing<T>& p = a.sp1;
+    const Spacing<T>& q = a.sp2;
+    a.scaled = p.pow2x && p.pow2y && q.pow2x && q.pow2y && p.inv2dx == p.inv2dy && q.inv2dx == q.inv2dy &&
+               p.inv2dx == q.inv2dx;
+    if (!a.scaled) return;
+    const T s = p.inv2dx;
+    a.c_half *= s;
+    a.c_dt *= s;
+    a.c_dt6 *= s;
+    a.coriolis_f /= s;
+}
 
 template <typename T>
 __host__ __device__ inline void fused_rows(const FusedArgs<T>& a, int i, int& y0, int& y1) {

@@ -56,7 +56,7 @@ __device__ __forceinline__ void publish(T* colp, const V3<T>& v) {
 // j+1 (down) and the published row j (x-neighbours, quantity Q). YCLAMP: the segment
 // touches a global y edge, where the reference clamps j-1 / j+1 to j
 // (weather_simulation.cpp:512-513).
-template <bool POW2, bool YCLAMP, int NST, int Q, typename T>
+template <int POW2, bool YCLAMP, int NST, int Q, typename T>
 __device__ __forceinline__ V3<T> stage_tend(const T* lcol, int j, const Geom& g, const V3<T>& up, const V3<T>& mid,
                                             const V3<T>& down, const Spacing<T>& sp, T grav, T cor) {
     constexpr int kCs = Lds<T, NST>::kCs;
@@ -82,7 +82,7 @@ constexpr int kU = 8;   // march unroll = y ring length
 #define WS_FUSED_MINW 1
 #endif
 
-template <typename T, int NST, bool POW2>
+template <typename T, int NST, int POW2>
 __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(FusedArgs<T> a, Geom g) {
     // All per-lane state lives in rotating register rings indexed by the march phase P
     // (compile-time): the body is instantiated for P = 0..kU-1, so ring "shifts" are renames,
@@ -286,10 +286,11 @@ hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, 
         return hipErrorInvalidValue;
     const dim3 grid((g.W + out_w - 1) / out_w, a.seg_n, g.L);
     const dim3 block(kFusedCols);
-    const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
+    const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
 #define WS_FUSED_LAUNCH(N)                                                                               \
-    if (pow2) hipLaunchKernelGGL((fused_step_kernel<T, N, true>), grid, block, 0, s, a, g);              \
-    else hipLaunchKernelGGL((fused_step_kernel<T, N, false>), grid, block, 0, s, a, g);
+    if (sp_mode == kSpScaled) hipLaunchKernelGGL((fused_step_kernel<T, N, kSpScaled>), grid, block, 0, s, a, g); \
+    else if (sp_mode == kSpMul) hipLaunchKernelGGL((fused_step_kernel<T, N, kSpMul>), grid, block, 0, s, a, g); \
+    else hipLaunchKernelGGL((fused_step_kernel<T, N, kSpDiv>), grid, block, 0, s, a, g);
     switch (nstages) {
         case 1: WS_FUSED_LAUNCH(1) break;
         case 2: WS_FUSED_LAUNCH(2) break;

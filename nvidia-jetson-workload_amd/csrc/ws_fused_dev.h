@@ -85,13 +85,17 @@ struct V3 {
     VT u, v, h;
 };
 
-template <bool POW2, typename VT, typename T>
+// Central difference, per spacing mode (ws_fused.h, fused_sp_mode): the reference's
+// (ar - al) / (2.0f * d); the same times the exact reciprocal when 2d is a power of two;
+// or, for scaled tendencies, the raw difference (the 1/(2d) factor rides on the constants).
+template <int MODE, typename VT, typename T>
 __device__ __forceinline__ VT cdiff(VT ar, VT al, T two_d, T inv) {
-    if constexpr (POW2) return (ar - al) * inv;  // exact: inv is a power of two
+    if constexpr (MODE == kSpScaled) return ar - al;
+    else if constexpr (MODE == kSpMul) return (ar - al) * inv;  // exact: inv is a power of two
     else return (ar - al) / two_d;
 }
 
-template <bool POW2, typename VT, typename T>
+template <int POW2, typename VT, typename T>
 __device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V3<VT>& r, const V3<VT>& t,
                                        const V3<VT>& b, const Spacing<T>& sp, T g, T f) {
     const VT u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);

@@ -30,7 +30,7 @@ constexpr int kUMax = unroll_for(WS_DPP_PF) > 16 ? unroll_for(WS_DPP_PF) : 16;
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
 // XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
 // the neighbour index to the cell itself (weather_simulation.cpp:510-513).
-template <bool POW2, bool XCLAMP, bool YCLAMP, typename T>
+template <int POW2, bool XCLAMP, bool YCLAMP, typename T>
 __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
                                             const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav,
                                             T cor) {
@@ -67,7 +67,7 @@ constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 
 // order LDS reads after LDS-DMA writes, so the kernel waits itself: every body issues
 // exactly 3 stores and every kG-th body 3 DMAs, hence a fixed count of younger vector-
 // memory ops at each wait (kWaitN below).
-template <typename T, int NST, bool POW2, int PF>
+template <typename T, int NST, int POW2, int PF>
 __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
     constexpr bool kDma = PF == 0;
@@ -327,15 +327,17 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 3 * kUMax) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblocks), block(kWave);
-    const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
+    const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
 #define WS_DPP_GO(N, P2, PF) hipLaunchKernelGGL((fused_dpp_kernel<T, N, P2, PF>), grid, block, 0, s, a, g, nstrips, nsegs)
 #define WS_DPP_LAUNCH(N)                     \
     if (dma) {                                  \
-        if (pow2) WS_DPP_GO(N, true, 0);        \
-        else WS_DPP_GO(N, false, 0);            \
+        if (sp_mode == kSpScaled) WS_DPP_GO(N, kSpScaled, 0);     \
+        else if (sp_mode == kSpMul) WS_DPP_GO(N, kSpMul, 0);      \
+        else WS_DPP_GO(N, kSpDiv, 0);                             \
     } else {                                    \
-        if (pow2) WS_DPP_GO(N, true, WS_DPP_PF); \
-        else WS_DPP_GO(N, false, WS_DPP_PF);    \
+        if (sp_mode == kSpScaled) WS_DPP_GO(N, kSpScaled, WS_DPP_PF); \
+        else if (sp_mode == kSpMul) WS_DPP_GO(N, kSpMul, WS_DPP_PF);  \
+        else WS_DPP_GO(N, kSpDiv, WS_DPP_PF);                         \
     }
     switch (nstages) {
         case 1: WS_DPP_LAUNCH(1) break;

@@ -55,7 +55,7 @@ struct EdgeCols {
 };
 
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
-template <bool POW2, bool XCLAMP, bool YCLAMP, typename T>
+template <int POW2, bool XCLAMP, bool YCLAMP, typename T>
 __device__ __forceinline__ V3<P2<T>> stage_tend(const EdgeCols& e, int j, const Geom& g, const V3<P2<T>>& up,
                                                 const V3<P2<T>>& mid, const V3<P2<T>>& down, const Spacing<T>& sp,
                                                 T grav, T cor) {
@@ -83,7 +83,7 @@ __device__ __forceinline__ V3<P2<T>> stage_tend(const EdgeCols& e, int j, const 
 #define WS_X2_MINW 1
 #endif
 
-template <typename T, int NST, bool POW2>
+template <typename T, int NST, int POW2>
 __global__ __launch_bounds__(kWave, WS_X2_MINW) void fused_x2_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                       int nsegs) {
     using VT = P2<T>;
@@ -322,10 +322,13 @@ hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& 
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
     if (g.pitch % 2 != 0) return hipErrorInvalidValue;  // column pairs stay 2-element aligned
     const dim3 grid((unsigned)nblocks), block(kWave);
-    const bool pow2 = a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y;
+    const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
 #define WS_X2_LAUNCH(N)                                                                                   \
-    if (pow2) hipLaunchKernelGGL((fused_x2_kernel<T, N, true>), grid, block, 0, s, a, g, nstrips, nsegs);  \
-    else hipLaunchKernelGGL((fused_x2_kernel<T, N, false>), grid, block, 0, s, a, g, nstrips, nsegs);
+    if (sp_mode == kSpScaled)                                                                              \
+        hipLaunchKernelGGL((fused_x2_kernel<T, N, kSpScaled>), grid, block, 0, s, a, g, nstrips, nsegs);   \
+    else if (sp_mode == kSpMul)                                                                            \
+        hipLaunchKernelGGL((fused_x2_kernel<T, N, kSpMul>), grid, block, 0, s, a, g, nstrips, nsegs);      \
+    else hipLaunchKernelGGL((fused_x2_kernel<T, N, kSpDiv>), grid, block, 0, s, a, g, nstrips, nsegs);
     switch (nstages) {
         case 1: WS_X2_LAUNCH(1) break;
         case 2: WS_X2_LAUNCH(2) break;

@@ -355,6 +355,9 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
+    // opt-in scaled tendencies (ws_fused.h): not bit-exact in the subnormal range
+    static const bool scaled_ok = env_int("WS_SCALED", 0) != 0;
+    if (scaled_ok) ws::scale_tendencies(a);
     const ws::Geom g = c->geom();
     switch (s->kernel) {
         case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
