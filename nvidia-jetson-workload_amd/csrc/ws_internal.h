@@ -59,6 +59,9 @@ hipError_t launch_diagnostics(const T* u, const T* v, T* vort, T* div, const Spa
 // out = in + c * tend_const   (PE T/P stale-tendency update, weather_simulation.cpp:201-214)
 template <typename T>
 hipError_t launch_affine(T* out, const T* in, T c, T tend, const Geom& g, hipStream_t s);
+// both PE updates in one pass: oT = iT + cT, oP = iP + cP (cX = dt * tendency, rounded in T)
+template <typename T>
+hipError_t launch_affine2(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP, const Geom& g, hipStream_t s);
 
 // fill all rows [0,H) of all levels with value
 template <typename T>

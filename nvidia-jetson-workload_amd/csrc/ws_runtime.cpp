@@ -226,6 +226,11 @@ struct ws_sim {
     ws_metrics_t metrics{};
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // PE: the T / P update runs on a second stream beside the stencil kernels (independent
+    // fields, see run_steps); joined with the main stream at the start and end of every run
+    hipStream_t aux = nullptr;
+    hipEvent_t aux_in = nullptr, aux_out = nullptr;
+    bool aux_active = false;
     double last_ms = 0.0;
     int64_t last_launches = 0;
     ws::KernelTimer timer;
@@ -421,10 +426,13 @@ void step_end(ws_sim* s) {
     }
     if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
         // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
+        // (`dt_ * tendency` has the same operands in every cell: one rounding, done here)
         const ws::Geom g = c->geom();
-        WS_HIP_CHECK(ws::launch_affine<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], dt, T(288.15f), g, s->stream));
-        WS_HIP_CHECK(ws::launch_affine<T>((T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], dt, T(1013.25f), g, s->stream));
-        s->last_launches += 2;
+        const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
+        WS_HIP_CHECK(ws::launch_affine2<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], cT,
+                                           (T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], cP, g,
+                                           s->aux_active ? s->aux : s->stream));
+        s->last_launches += 1;
     }
     s->cur = 1 - s->cur;
     s->slot[s->cur]->diag_pending = true;  // step() ends with calculateDiagnostics (:149)
@@ -565,11 +573,29 @@ void run_steps(ws_sim* s, int k) {
     // otherwise (halo exchanges or PE T/P updates share the stream) time every 8th launch
     s->timer.sample_period(span || !use_fused(s) ? 1 : 8);
     WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
+    // PE: T / P updates on the aux stream, in step order there, concurrent with the stencil
+    // kernels (they touch neither u, v, h nor each other's inputs across streams); the aux
+    // stream starts after everything queued so far and the main stream waits for it at the end
+    s->aux_active = k > 0 && s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS && env_int("WS_PE_AUX", 1) != 0;
+    if (s->aux_active) {
+        if (!s->aux) {
+            WS_HIP_CHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+            WS_HIP_CHECK(hipEventCreateWithFlags(&s->aux_in, hipEventDisableTiming));
+            WS_HIP_CHECK(hipEventCreateWithFlags(&s->aux_out, hipEventDisableTiming));
+        }
+        WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
+        WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
+    }
     for (int i = 0; i < k; ++i) {
         if (s->dtype == WS_F64) enqueue_step<double>(s);
         else enqueue_step<float>(s);
         s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
         s->step++;
+    }
+    if (s->aux_active) {
+        WS_HIP_CHECK(hipEventRecord(s->aux_out, s->aux));
+        WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->aux_out, 0));
+        s->aux_active = false;
     }
     WS_HIP_CHECK(hipEventRecord(s->ev1, s->stream));
     if (k > 0 && s->comm) {
@@ -598,8 +624,9 @@ void run_steps(ws_sim* s, int k) {
 void sim_free(ws_sim* s) {
     for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
         if (g) { grid_free(g); delete g; }
-    for (hipEvent_t e : {s->ev0, s->ev1})
+    for (hipEvent_t e : {s->ev0, s->ev1, s->aux_in, s->aux_out})
         if (e) (void)hipEventDestroy(e);
+    if (s->aux) (void)hipStreamDestroy(s->aux);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
     delete s->comm;
     delete s;
