@@ -233,11 +233,36 @@ int ws_slab_partition(int32_t height, int32_t rank, int32_t nranks, int32_t* row
 int ws_sim_comm_allreduce_max(ws_sim_t* sim, double value, double* out);
 int ws_sim_comm_barrier(ws_sim_t* sim);
 
+/* ---- physics-mode barotropic vorticity model (new) ------------------ */
+/* BASELINE config C3 names a "Jacobian + Laplacian" barotropic model; the reference has
+ * none (its Barotropic model runs the SWE tendencies, weather_simulation.cpp:542-560, which
+ * ws_sim_* reproduces bit for bit). This is that model, defined by oracle/bvort_oracle.py:
+ * doubly periodic, d(zeta)/dt = -J(psi, zeta) - beta psi_x + nu lap(zeta), lap(psi) = zeta
+ * (Arakawa Jacobian, spectral Poisson via hipFFT). From cfg it reads grid_width/height, dx,
+ * dy, dt, beta, viscosity (the SimulationConfig fields the reference never reads,
+ * weather_sim.hpp:176-178), integration_method (Euler / RK2 / classical RK4; others run
+ * Euler), double_precision and device_id. */
+typedef struct ws_bvort ws_bvort_t;
+int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out);
+int ws_bvort_destroy(ws_bvort_t* model);
+/* (height, width) C-contiguous host array, fp32 or fp64 (converted like a C cast) */
+int ws_bvort_set_vorticity(ws_bvort_t* model, const void* host, int32_t height, int32_t width, int32_t dtype);
+/* which: 0 vorticity, 1 streamfunction, 2 u = -psi_y, 3 v = psi_x; dtype = the model's */
+int ws_bvort_get_field(ws_bvort_t* model, int32_t which, void* host, int32_t height, int32_t width, int32_t dtype);
+/* n steps on the device, one host synchronisation at the end */
+int ws_bvort_run(ws_bvort_t* model, int32_t num_steps);
+int ws_bvort_get_state(const ws_bvort_t* model, double* time, int32_t* step, double* last_run_ms,
+                       int64_t* last_run_launches);
+
 /* ---- per-kernel timing (measurement) --------------------------------------------- */
-/* When enabled, every stage kernel of ws_sim_run / ws_sim_step is bracketed by hipEvents
- * on the simulation's stream. kind = stage index within the step (0..3 for RK4). The
- * statistics reset when timing is (re-)enabled. bytes_per_launch is the algorithmic
- * HBM traffic of one launch (SURVEY §8(d) words x cells x element size).
+/* When enabled, ws_sim_run / ws_sim_step time their kernels with hipEvents on the
+ * simulation's stream: a run whose steps are one fused launch each (and nothing else on
+ * the stream) is timed as a whole and attributed per launch (no events between the
+ * launches); otherwise every 8th fused launch (or every per-stage kernel of the fallback
+ * path) is bracketed by events. kind = stage index within the step (0..3 for RK4; 0 for
+ * the fused kernel). The statistics reset when timing is (re-)enabled. bytes_per_launch
+ * is the algorithmic HBM traffic of one launch (SURVEY §8(d) words x cells x element size;
+ * the fused kernel: 6 words).
  * enable = 0: off; 1: on; n > 1: on, with events for n launches created up front. */
 int ws_sim_set_kernel_timing(ws_sim_t* sim, int32_t enable);
 int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, double* total_ms,

@@ -1,0 +1,423 @@
+// Physics-mode barotropic vorticity model (BASELINE config C3's "Jacobian +
+// Laplacian stencil"). The reference has no such model -- its Barotropic model runs the
+// shallow-water tendencies (weather_simulation.cpp:542-560) -- so this is a new model with
+// its own oracle (oracle/bvort_oracle.py, pinned against analytic solutions of the discrete
+// system). Doubly periodic W x H grid:
+//     d(zeta)/dt = -J(psi, zeta) - beta d(psi)/dx + nu lap(zeta),   lap(psi) = zeta
+// J = Arakawa (1966) 9-point Jacobian; the Poisson inverse is spectral (hipFFT R2C / C2R
+// around a diagonal scale by the 5-point Laplacian's eigenvalues); the config fields
+// `beta` and `viscosity` (weather_sim.hpp:176-178, never read by the reference) are the
+// parameters. Euler, RK2 midpoint and classical RK4.
+//
+// Per RK stage: R2C(zeta_s) -> scale -> C2R -> psi_s, then one fused stencil kernel computes
+// the tendency at every cell from LDS tiles of psi_s and zeta_s (1-cell periodic halo) and
+// applies the stage update (and the RK4 accumulator) in the same pass.
+#include <hip/hip_runtime.h>
+#include <hipfft/hipfft.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ws_abi.h"
+#include "ws_hip.h"
+
+namespace ws {
+namespace {
+
+constexpr int kTX = 64;  // tile columns (one wave wide)
+constexpr int kTY = 16;  // tile rows (4 per thread, 4 waves)
+constexpr int kBY = 4;
+
+template <typename T>
+struct BvArgs {
+    const T* zin;   // stage input zeta (stencil)
+    const T* psi;   // its streamfunction
+    const T* z0;    // zeta at the start of the step
+    T* zout;        // z0 + c * k
+    T* acc;         // RK4: sum of weighted tendencies
+    int W, H;
+    T c;            // stage coefficient
+    T w;            // accumulator weight
+    int acc_mode;   // 0 none, 1 acc = w k, 2 acc += w k, 3 final: zout = z0 + c (acc + k)
+    T inv12dxdy, inv2dx, idx2, idy2, beta, nu;
+};
+
+__device__ __forceinline__ int wrap(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+
+template <typename T>
+__global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
+    __shared__ T P[kTY + 2][kTX + 2];
+    __shared__ T Z[kTY + 2][kTX + 2];
+    const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+    const int tid = threadIdx.y * kTX + threadIdx.x;
+    for (int i = tid; i < (kTY + 2) * (kTX + 2); i += kTX * kBY) {
+        const int ly = i / (kTX + 2), lx = i % (kTX + 2);
+        // (x0 + lx - 1) lies in [-1, W + 64]: one wrap step is not enough past the grid's
+        // end for narrow grids, so reduce fully
+        int gx = (x0 + lx - 1) % a.W;
+        if (gx < 0) gx += a.W;
+        int gy = (y0 + ly - 1) % a.H;
+        if (gy < 0) gy += a.H;
+        const int64_t o = (int64_t)gy * a.W + gx;
+        P[ly][lx] = a.psi[o];
+        Z[ly][lx] = a.zin[o];
+    }
+    __syncthreads();
+    const int lx = threadIdx.x + 1;
+    const int x = x0 + threadIdx.x;
+    if (x >= a.W) return;
+#pragma unroll
+    for (int r = 0; r < kTY / kBY; ++r) {
+        const int ly = threadIdx.y + r * kBY + 1;
+        const int y = y0 + ly - 1;
+        if (y >= a.H) break;
+        // e / w = x +- 1, n / s = y +- 1 (n = the next row in memory, as oracle/bvort_oracle.py)
+        const T pc = P[ly][lx], pe = P[ly][lx + 1], pw = P[ly][lx - 1], pn = P[ly + 1][lx], ps = P[ly - 1][lx];
+        const T pne = P[ly + 1][lx + 1], pnw = P[ly + 1][lx - 1], pse = P[ly - 1][lx + 1], psw = P[ly - 1][lx - 1];
+        const T zc = Z[ly][lx], ze = Z[ly][lx + 1], zw = Z[ly][lx - 1], zn = Z[ly + 1][lx], zs = Z[ly - 1][lx];
+        const T zne = Z[ly + 1][lx + 1], znw = Z[ly + 1][lx - 1], zse = Z[ly - 1][lx + 1], zsw = Z[ly - 1][lx - 1];
+        (void)pc;
+        const T jpp = (pe - pw) * (zn - zs) - (pn - ps) * (ze - zw);
+        const T jpx = pe * (zne - zse) - pw * (znw - zsw) - pn * (zne - znw) + ps * (zse - zsw);
+        const T jxp = zn * (pne - pnw) - zs * (pse - psw) - ze * (pne - pse) + zw * (pnw - psw);
+        T k = -((jpp + jpx + jxp) * a.inv12dxdy);
+        k = k - a.beta * ((pe - pw) * a.inv2dx);
+        k = k + a.nu * ((ze + zw - T(2) * zc) * a.idx2 + (zn + zs - T(2) * zc) * a.idy2);
+        const int64_t o = (int64_t)y * a.W + x;
+        const T z0 = a.z0[o];
+        switch (a.acc_mode) {
+            case 0: a.zout[o] = z0 + a.c * k; break;
+            case 1: a.zout[o] = z0 + a.c * k; a.acc[o] = a.w * k; break;
+            case 2: a.zout[o] = z0 + a.c * k; a.acc[o] = a.acc[o] + a.w * k; break;
+            default: a.zout[o] = z0 + a.c * (a.acc[o] + k); break;
+        }
+    }
+}
+
+// spec[l][k] *= norm / lambda(k, l), lambda = ax[k] + ay[l]; the (0, 0) mode (lambda = 0,
+// the domain mean) is set to 0.
+template <typename T, typename C>
+__global__ __launch_bounds__(256) void bv_spectral_kernel(C* spec, const T* ax, const T* ay, int nk, int H, T norm) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int l = blockIdx.y;
+    if (k >= nk) return;
+    const int64_t o = (int64_t)l * nk + k;
+    const T lam = ax[k] + ay[l];
+    const T m = (k == 0 && l == 0) ? T(0) : norm / lam;
+    C v = spec[o];
+    v.x *= m;
+    v.y *= m;
+    spec[o] = v;
+}
+
+// u = -d(psi)/dy, v = d(psi)/dx (centred, periodic)
+template <typename T>
+__global__ __launch_bounds__(256) void bv_velocity_kernel(const T* psi, T* u, T* v, int W, int H, T inv2dx,
+                                                          T inv2dy) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const int64_t o = (int64_t)y * W + x;
+    const T pn = psi[(int64_t)wrap(y + 1, H) * W + x], ps = psi[(int64_t)wrap(y - 1, H) * W + x];
+    const T pe = psi[(int64_t)y * W + wrap(x + 1, W)], pw = psi[(int64_t)y * W + wrap(x - 1, W)];
+    u[o] = -((pn - ps) * inv2dy);
+    v[o] = (pe - pw) * inv2dx;
+}
+
+void hck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw AbiError(WS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+void fck(hipfftResult r, const char* what) {
+    if (r != HIPFFT_SUCCESS) throw AbiError(WS_ERR_DEVICE, std::string(what) + ": hipFFT error " + std::to_string((int)r));
+}
+
+}  // namespace
+}  // namespace ws
+
+struct ws_bvort {
+    int W = 0, H = 0, dtype = WS_F32, device = 0, method = WS_RK4;
+    double dx = 1, dy = 1, dt = 0.01, beta = 0, nu = 0;
+    double time = 0;
+    int32_t step = 0;
+    hipStream_t stream = nullptr;
+    hipfftHandle r2c = 0, c2r = 0;
+    bool have_r2c = false, have_c2r = false;
+    void* z[2] = {nullptr, nullptr};
+    void *A = nullptr, *B = nullptr, *psi = nullptr, *acc = nullptr, *spec = nullptr, *ax = nullptr, *ay = nullptr;
+    void *u = nullptr, *v = nullptr;
+    int cur = 0;
+    bool psi_current = false;  // psi holds the streamfunction of z[cur]
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0;
+    int64_t launches = 0;
+
+    size_t es() const { return dtype == WS_F64 ? 8 : 4; }
+    size_t cells() const { return (size_t)W * H; }
+};
+
+namespace ws {
+namespace {
+
+void bv_free(ws_bvort* b) {
+    for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay, b->u, b->v})
+        if (p) (void)hipFree(p);
+    if (b->have_r2c) hipfftDestroy(b->r2c);
+    if (b->have_c2r) hipfftDestroy(b->c2r);
+    for (hipEvent_t e : {b->ev0, b->ev1})
+        if (e) (void)hipEventDestroy(e);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+template <typename T>
+void upload_eigen(ws_bvort* b) {
+    const int nk = b->W / 2 + 1;
+    std::vector<T> ax(nk), ay(b->H);
+    const double pi = 3.14159265358979323846;
+    for (int k = 0; k < nk; ++k) ax[k] = (T)((2.0 * std::cos(2.0 * pi * k / b->W) - 2.0) / (b->dx * b->dx));
+    for (int l = 0; l < b->H; ++l) ay[l] = (T)((2.0 * std::cos(2.0 * pi * l / b->H) - 2.0) / (b->dy * b->dy));
+    hck(hipMemcpy(b->ax, ax.data(), nk * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+    hck(hipMemcpy(b->ay, ay.data(), b->H * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+// psi = lap^-1 zin (spectral), on the model's stream
+template <typename T>
+void poisson(ws_bvort* b, const void* zin) {
+    const int nk = b->W / 2 + 1;
+    if constexpr (sizeof(T) == 8) {
+        fck(hipfftExecD2Z(b->r2c, (hipfftDoubleReal*)const_cast<void*>(zin), (hipfftDoubleComplex*)b->spec), "D2Z");
+        hipLaunchKernelGGL((bv_spectral_kernel<double, double2>), dim3((nk + 255) / 256, b->H), dim3(256), 0,
+                           b->stream, (double2*)b->spec, (const double*)b->ax, (const double*)b->ay, nk, b->H,
+                           1.0 / ((double)b->W * b->H));
+        hck(hipGetLastError(), "bv_spectral_kernel");
+        fck(hipfftExecZ2D(b->c2r, (hipfftDoubleComplex*)b->spec, (hipfftDoubleReal*)b->psi), "Z2D");
+    } else {
+        fck(hipfftExecR2C(b->r2c, (hipfftReal*)const_cast<void*>(zin), (hipfftComplex*)b->spec), "R2C");
+        hipLaunchKernelGGL((bv_spectral_kernel<float, float2>), dim3((nk + 255) / 256, b->H), dim3(256), 0,
+                           b->stream, (float2*)b->spec, (const float*)b->ax, (const float*)b->ay, nk, b->H,
+                           (float)(1.0 / ((double)b->W * b->H)));
+        hck(hipGetLastError(), "bv_spectral_kernel");
+        fck(hipfftExecC2R(b->c2r, (hipfftComplex*)b->spec, (hipfftReal*)b->psi), "C2R");
+    }
+    b->launches += 3;
+}
+
+template <typename T>
+void stage(ws_bvort* b, const void* zin, void* zout, T c, T w, int acc_mode) {
+    poisson<T>(b, zin);
+    BvArgs<T> a{};
+    a.zin = (const T*)zin;
+    a.psi = (const T*)b->psi;
+    a.z0 = (const T*)b->z[b->cur];
+    a.zout = (T*)zout;
+    a.acc = (T*)b->acc;
+    a.W = b->W;
+    a.H = b->H;
+    a.c = c;
+    a.w = w;
+    a.acc_mode = acc_mode;
+    a.inv12dxdy = (T)(1.0 / (12.0 * b->dx * b->dy));
+    a.inv2dx = (T)(1.0 / (2.0 * b->dx));
+    a.idx2 = (T)(1.0 / (b->dx * b->dx));
+    a.idy2 = (T)(1.0 / (b->dy * b->dy));
+    a.beta = (T)b->beta;
+    a.nu = (T)b->nu;
+    const dim3 grid((b->W + kTX - 1) / kTX, (b->H + kTY - 1) / kTY), block(kTX, kBY);
+    hipLaunchKernelGGL((bv_stage_kernel<T>), grid, block, 0, b->stream, a);
+    hck(hipGetLastError(), "bv_stage_kernel");
+    b->launches += 1;
+}
+
+template <typename T>
+void enqueue_step(ws_bvort* b) {
+    const T dt = (T)b->dt;
+    void* z0 = b->z[b->cur];
+    void* z1 = b->z[1 - b->cur];
+    switch (b->method) {
+        case WS_RK2:
+            stage<T>(b, z0, b->A, T(0.5) * dt, T(0), 0);
+            stage<T>(b, b->A, z1, dt, T(0), 0);
+            break;
+        case WS_RK4:
+            stage<T>(b, z0, b->A, T(0.5) * dt, T(1), 1);
+            stage<T>(b, b->A, b->B, T(0.5) * dt, T(2), 2);
+            stage<T>(b, b->B, b->A, dt, T(2), 2);
+            stage<T>(b, b->A, z1, dt / T(6), T(0), 3);
+            break;
+        default:  // Euler
+            stage<T>(b, z0, z1, dt, T(0), 0);
+            break;
+    }
+    b->cur = 1 - b->cur;
+    b->psi_current = false;
+}
+
+template <typename T>
+void convert_copy(void* dst, int dst_dtype, const void* src, int src_dtype, size_t n) {
+    (void)dst_dtype;
+    T* d = (T*)dst;
+    if (src_dtype == WS_F64) {
+        const double* s = (const double*)src;
+        for (size_t i = 0; i < n; ++i) d[i] = (T)s[i];
+    } else {
+        const float* s = (const float*)src;
+        for (size_t i = 0; i < n; ++i) d[i] = (T)s[i];
+    }
+}
+
+}  // namespace
+}  // namespace ws
+
+using ws::AbiError;
+
+extern "C" {
+
+int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
+    return ws::abi_guarded([&] {
+        if (!cfg || !out) throw AbiError(WS_ERR_INVALID, "null argument");
+        if (cfg->grid_width < 3 || cfg->grid_height < 3)
+            throw AbiError(WS_ERR_INVALID, "barotropic vorticity model needs a grid of at least 3 x 3");
+        if (!(cfg->dx > 0 && cfg->dy > 0)) throw AbiError(WS_ERR_INVALID, "Grid spacing must be positive");
+        ws::abi_set_device(cfg->device_id);
+        ws_bvort* b = new ws_bvort;
+        b->W = cfg->grid_width;
+        b->H = cfg->grid_height;
+        b->dtype = cfg->double_precision ? WS_F64 : WS_F32;
+        b->device = cfg->device_id;
+        b->method = cfg->integration_method == WS_RK2 ? WS_RK2 : cfg->integration_method == WS_RK4 ? WS_RK4 : WS_EULER;
+        b->dx = cfg->dx;
+        b->dy = cfg->dy;
+        b->dt = cfg->dt;
+        b->beta = cfg->beta;
+        b->nu = cfg->viscosity;
+        try {
+            ws::hck(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), "hipStreamCreate");
+            ws::hck(hipEventCreate(&b->ev0), "hipEventCreate");
+            ws::hck(hipEventCreate(&b->ev1), "hipEventCreate");
+            const size_t fb = b->cells() * b->es();
+            for (void** p : {&b->z[0], &b->z[1], &b->A, &b->B, &b->psi, &b->acc})
+                ws::hck(hipMalloc(p, fb), "hipMalloc");
+            const int nk = b->W / 2 + 1;
+            ws::hck(hipMalloc(&b->spec, (size_t)nk * b->H * 2 * b->es()), "hipMalloc");
+            ws::hck(hipMalloc(&b->ax, (size_t)nk * b->es()), "hipMalloc");
+            ws::hck(hipMalloc(&b->ay, (size_t)b->H * b->es()), "hipMalloc");
+            for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc})
+                ws::hck(hipMemset(p, 0, fb), "hipMemset");
+            const bool f64 = b->dtype == WS_F64;
+            ws::fck(hipfftPlan2d(&b->r2c, b->H, b->W, f64 ? HIPFFT_D2Z : HIPFFT_R2C), "hipfftPlan2d");
+            b->have_r2c = true;
+            ws::fck(hipfftPlan2d(&b->c2r, b->H, b->W, f64 ? HIPFFT_Z2D : HIPFFT_C2R), "hipfftPlan2d");
+            b->have_c2r = true;
+            ws::fck(hipfftSetStream(b->r2c, b->stream), "hipfftSetStream");
+            ws::fck(hipfftSetStream(b->c2r, b->stream), "hipfftSetStream");
+            if (f64) ws::upload_eigen<double>(b);
+            else ws::upload_eigen<float>(b);
+        } catch (...) {
+            ws::bv_free(b);
+            throw;
+        }
+        *out = b;
+    });
+}
+
+int ws_bvort_destroy(ws_bvort_t* b) {
+    return ws::abi_guarded([&] {
+        if (!b) return;
+        (void)hipSetDevice(b->device);
+        (void)hipStreamSynchronize(b->stream);
+        ws::bv_free(b);
+    });
+}
+
+int ws_bvort_set_vorticity(ws_bvort_t* b, const void* host, int32_t height, int32_t width, int32_t dtype) {
+    return ws::abi_guarded([&] {
+        if (!b || !host) throw AbiError(WS_ERR_INVALID, "null argument");
+        if (height != b->H || width != b->W) throw AbiError(WS_ERR_SHAPE, "vorticity array shape mismatch");
+        if (dtype != WS_F32 && dtype != WS_F64) throw AbiError(WS_ERR_INVALID, "bad dtype");
+        ws::abi_set_device(b->device);
+        std::vector<char> buf(b->cells() * b->es());
+        if (b->dtype == WS_F64) ws::convert_copy<double>(buf.data(), b->dtype, host, dtype, b->cells());
+        else ws::convert_copy<float>(buf.data(), b->dtype, host, dtype, b->cells());
+        ws::hck(hipStreamSynchronize(b->stream), "hipStreamSynchronize");
+        ws::hck(hipMemcpy(b->z[b->cur], buf.data(), buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        b->psi_current = false;
+    });
+}
+
+// which: 0 vorticity, 1 streamfunction, 2 u, 3 v (of the current state)
+int ws_bvort_get_field(ws_bvort_t* b, int32_t which, void* host, int32_t height, int32_t width, int32_t dtype) {
+    return ws::abi_guarded([&] {
+        if (!b || !host) throw AbiError(WS_ERR_INVALID, "null argument");
+        if (which < 0 || which > 3) throw AbiError(WS_ERR_INVALID, "bad field id");
+        if (height != b->H || width != b->W) throw AbiError(WS_ERR_SHAPE, "array shape mismatch");
+        if (dtype != b->dtype) throw AbiError(WS_ERR_INVALID, "dtype must match the model precision");
+        ws::abi_set_device(b->device);
+        const void* src = b->z[b->cur];
+        if (which >= 1) {
+            if (!b->psi_current) {
+                if (b->dtype == WS_F64) ws::poisson<double>(b, b->z[b->cur]);
+                else ws::poisson<float>(b, b->z[b->cur]);
+                b->psi_current = true;
+            }
+            src = b->psi;
+            if (which >= 2) {
+                const size_t fb = b->cells() * b->es();
+                if (!b->u) ws::hck(hipMalloc(&b->u, fb), "hipMalloc");
+                if (!b->v) ws::hck(hipMalloc(&b->v, fb), "hipMalloc");
+                const dim3 grid((b->W + 255) / 256, b->H);
+                if (b->dtype == WS_F64)
+                    hipLaunchKernelGGL((ws::bv_velocity_kernel<double>), grid, dim3(256), 0, b->stream,
+                                       (const double*)b->psi, (double*)b->u, (double*)b->v, b->W, b->H,
+                                       1.0 / (2.0 * b->dx), 1.0 / (2.0 * b->dy));
+                else
+                    hipLaunchKernelGGL((ws::bv_velocity_kernel<float>), grid, dim3(256), 0, b->stream,
+                                       (const float*)b->psi, (float*)b->u, (float*)b->v, b->W, b->H,
+                                       (float)(1.0 / (2.0 * b->dx)), (float)(1.0 / (2.0 * b->dy)));
+                ws::hck(hipGetLastError(), "bv_velocity_kernel");
+                src = which == 2 ? b->u : b->v;
+            }
+        }
+        ws::hck(hipStreamSynchronize(b->stream), "hipStreamSynchronize");
+        ws::hck(hipMemcpy(host, src, b->cells() * b->es(), hipMemcpyDeviceToHost), "hipMemcpy");
+    });
+}
+
+int ws_bvort_run(ws_bvort_t* b, int32_t n) {
+    return ws::abi_guarded([&] {
+        if (!b) throw AbiError(WS_ERR_INVALID, "null model");
+        if (n <= 0) return;
+        ws::abi_set_device(b->device);
+        b->launches = 0;
+        ws::hck(hipEventRecord(b->ev0, b->stream), "hipEventRecord");
+        for (int i = 0; i < n; ++i) {
+            if (b->dtype == WS_F64) {
+                ws::enqueue_step<double>(b);
+                b->time += b->dt;
+            } else {
+                ws::enqueue_step<float>(b);
+                b->time = (double)((float)b->time + (float)b->dt);
+            }
+            b->step++;
+        }
+        ws::hck(hipEventRecord(b->ev1, b->stream), "hipEventRecord");
+        ws::hck(hipEventSynchronize(b->ev1), "hipEventSynchronize");
+        float ms = 0.f;
+        ws::hck(hipEventElapsedTime(&ms, b->ev0, b->ev1), "hipEventElapsedTime");
+        b->last_ms = ms;
+    });
+}
+
+int ws_bvort_get_state(const ws_bvort_t* b, double* time, int32_t* step, double* last_run_ms,
+                       int64_t* last_run_launches) {
+    return ws::abi_guarded([&] {
+        if (!b) throw AbiError(WS_ERR_INVALID, "null model");
+        if (time) *time = b->time;
+        if (step) *step = b->step;
+        if (last_run_ms) *last_run_ms = b->last_ms;
+        if (last_run_launches) *last_run_launches = b->launches;
+    });
+}
+
+}  // extern "C"

@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "ws_abi.h"
 #include "ws_comm.h"
 #include "ws_fused.h"
 #include "ws_ic.h"
@@ -46,6 +47,9 @@ int guarded(F&& f) {
         f();
         return WS_OK;
     } catch (const WsError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const ws::AbiError& e) {
         g_last_error = e.what();
         return e.code;
     } catch (const ws::CommError& e) {
@@ -1482,3 +1486,8 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
 }
 
 }  // extern "C"
+
+namespace ws {
+int abi_guarded(const std::function<void()>& f) { return guarded(f); }
+void abi_set_device(int device) { set_device(device); }
+}  // namespace ws

@@ -116,6 +116,12 @@ SIGNATURES = {
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
     "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
+    "ws_bvort_create": [ctypes.POINTER(ws_config_t), _PP],
+    "ws_bvort_destroy": [_P],
+    "ws_bvort_set_vorticity": [_P, _P, _I, _I, _I],
+    "ws_bvort_get_field": [_P, _I, _P, _I, _I, _I],
+    "ws_bvort_run": [_P, _I],
+    "ws_bvort_get_state": [_P, _PD, _PI, _PD, _PL],
 }
 _RESTYPES = {"ws_last_error": ctypes.c_char_p, "ws_config_default": None}
 

@@ -1,0 +1,110 @@
+"""Physics-mode barotropic vorticity model over libws_hip.so.
+
+BASELINE config C3 describes a barotropic "Jacobian + Laplacian" model. The reference has
+none: its `SimulationModel.Barotropic` runs the shallow-water tendencies
+(src/weather-sim/cpp/src/weather_simulation.cpp:542-560), which `WeatherSimulation`
+reproduces bit for bit. This class is the physical model that description names -- a new
+model, defined by oracle/bvort_oracle.py and checked against it and against analytic
+solutions (tests/test_bvort_oracle.py, tests/test_gpu_bvort.py):
+
+    d(zeta)/dt = -J(psi, zeta) - beta * d(psi)/dx + nu * lap(zeta),    lap(psi) = zeta
+
+on a doubly periodic grid: Arakawa 9-point Jacobian, 5-point Laplacian, spectral Poisson
+inverse (hipFFT), Euler / RK2 midpoint / classical RK4. It takes the reference's
+`SimulationConfig` and reads the fields the reference accepts but never uses: `beta` and
+`viscosity` (weather_sim.hpp:176-178).
+
+    cfg = SimulationConfig(); cfg.grid_width = cfg.grid_height = 2048
+    cfg.beta, cfg.viscosity, cfg.dt = 1e-3, 1e-4, 0.05
+    m = BarotropicVorticityModel(cfg)
+    m.set_vorticity(zeta0); m.run(100); u, v = m.get_velocity_field()
+"""
+import ctypes
+
+import numpy as np
+
+from ._native import WS_F32, WS_F64, check, lib
+
+_FIELDS = {"vorticity": 0, "streamfunction": 1, "u": 2, "v": 3}
+
+
+class BarotropicVorticityModel:
+    """One barotropic vorticity model on the device (no CPU path: fails without a GPU)."""
+
+    def __init__(self, config):
+        from .weather_simulation import SimulationConfig
+        if not isinstance(config, SimulationConfig):
+            raise TypeError("BarotropicVorticityModel expects a SimulationConfig")
+        self._cfg = config
+        raw = config._to_c()
+        h = ctypes.c_void_p()
+        check(lib.ws_bvort_create(ctypes.byref(raw), ctypes.byref(h)))
+        self._h = h
+        self.width, self.height = int(config.grid_width), int(config.grid_height)
+        self.dtype = np.float64 if config.double_precision else np.float32
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.ws_bvort_destroy(h)
+            self._h = None
+
+    # -- state ---------------------------------------------------------------------
+    def set_vorticity(self, zeta):
+        a = np.ascontiguousarray(zeta)
+        if a.ndim != 2:
+            raise RuntimeError("vorticity must be a 2-D (height, width) array")
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float64)
+        code = WS_F64 if a.dtype == np.float64 else WS_F32
+        check(lib.ws_bvort_set_vorticity(self._h, a.ctypes.data_as(ctypes.c_void_p), a.shape[0], a.shape[1], code))
+
+    def _get(self, which):
+        out = np.empty((self.height, self.width), dtype=self.dtype)
+        code = WS_F64 if self.dtype == np.float64 else WS_F32
+        check(lib.ws_bvort_get_field(self._h, _FIELDS[which], out.ctypes.data_as(ctypes.c_void_p), self.height,
+                                     self.width, code))
+        return out
+
+    def get_vorticity_field(self):
+        return self._get("vorticity")
+
+    def get_streamfunction(self):
+        return self._get("streamfunction")
+
+    def get_velocity_field(self):
+        """(u, v) = (-d(psi)/dy, d(psi)/dx), centred differences."""
+        return self._get("u"), self._get("v")
+
+    # -- stepping ------------------------------------------------------------------
+    def step(self):
+        self.run(1)
+
+    def run(self, num_steps):
+        check(lib.ws_bvort_run(self._h, int(num_steps)))
+        return int(num_steps)
+
+    def _state(self):
+        t, s, ms, n = ctypes.c_double(), ctypes.c_int32(), ctypes.c_double(), ctypes.c_int64()
+        check(lib.ws_bvort_get_state(self._h, ctypes.byref(t), ctypes.byref(s), ctypes.byref(ms), ctypes.byref(n)))
+        return t.value, s.value, ms.value, n.value
+
+    def get_current_time(self):
+        return self._state()[0]
+
+    def get_current_step(self):
+        return self._state()[1]
+
+    def last_run_stats(self):
+        """(device ms of the last run(), kernel + FFT launches it made)"""
+        _, _, ms, n = self._state()
+        return ms, n
+
+    # -- diagnostics (host reductions of fields already copied out) -----------------
+    def energy(self):
+        """Discrete kinetic energy -1/2 sum(psi * zeta): conserved by the Arakawa Jacobian."""
+        return -0.5 * float(np.sum(self.get_streamfunction().astype(np.float64) *
+                                   self.get_vorticity_field().astype(np.float64)))
+
+    def enstrophy(self):
+        return 0.5 * float(np.sum(self.get_vorticity_field().astype(np.float64) ** 2))

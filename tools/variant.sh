@@ -10,5 +10,5 @@ FLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../incl
 /opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/$NAME.o
 OBJS=$(ls _obj/*.o | grep -v "/${SRC}.o$")
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/variants/libws_hip_$NAME.so $OBJS _obj/var/$NAME.o \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+    -L/opt/rocm/lib -lrccl -lhipfft -Wl,-rpath,/opt/rocm/lib
 echo "built lib/variants/libws_hip_$NAME.so"
