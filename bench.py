@@ -51,6 +51,11 @@ CONFIGS = {
                      workload="C2 slab of 4: Shallow Water 4096x1024 fp64"),
     "c2_slab8": dict(W=4096, H=512, L=1, model=0, fp64=True, ic="jet_stream",
                      workload="C2 slab of 8: Shallow Water 4096x512 fp64"),
+    # C3 as BASELINE describes it ("Jacobian + Laplacian"): the physics-mode barotropic
+    # vorticity model (no reference semantics, see weather_sim/physics.py)
+    "c3p": dict(W=2048, H=2048, L=1, model=1, fp64=False, ic="rossby",
+                workload="C3 physics mode: barotropic vorticity (Arakawa Jacobian + Laplacian, hipFFT Poisson) "
+                         "2048x2048 fp32"),
 }
 METHODS = {"euler": 0, "rk2": 1, "rk4": 2}
 
@@ -142,6 +147,81 @@ def cpu_baseline(conf, method, budget_s=20.0):
                       f"OMP_NUM_THREADS={threads}"}
 
 
+def bvort_words_per_cell(method, W, H):
+    """Algorithmic traffic of one barotropic step in words per cell: per RK stage an R2C
+    (read W*H reals, write (W/2+1)*H complex), the spectral scale (read + write the
+    spectrum), a C2R (read the spectrum, write W*H reals) and the stage stencil (read zeta_s,
+    psi, zeta_0 [+ acc], write zeta_out [+ acc])."""
+    spec = 2.0 * (W // 2 + 1) * H / (W * H)  # complex spectrum, in real words per cell
+    fft = (1 + spec) + 2 * spec + (spec + 1)
+    stencil = {0: [4], 1: [4, 4], 2: [5, 6, 6, 5]}[method]
+    return sum(fft + s for s in stencil)
+
+
+def bench_bvort(args, conf, method, world):
+    """Physics-mode barotropic (config c3p): one process, the whole model on one GPU."""
+    import numpy as np
+    import torch
+    import weather_sim as ws
+    from oracle import bvort_oracle as bo
+
+    if world > 1:
+        raise SystemExit("c3p runs on one GPU (the spectral Poisson solve is not slab-decomposed)")
+    W, H = conf["W"], conf["H"]
+    cfg = ws.SimulationConfig()
+    cfg.grid_width, cfg.grid_height = W, H
+    cfg.integration_method = method
+    cfg.double_precision = conf["fp64"]
+    # beta small enough that the gravest Rossby mode (omega ~ beta W / 2 pi) stays inside
+    # RK4's stability region at this dt
+    cfg.dt, cfg.beta, cfg.viscosity = 0.05, 1e-3, 0.01
+    m = ws.BarotropicVorticityModel(cfg)
+    z0 = bo.rossby_mode(W, H, 1.0, 1.0, 5, 3, amp=1e-2) + bo.rossby_mode(W, H, 1.0, 1.0, 2, 7, amp=5e-3)
+    m.set_vorticity(z0)
+    if args.warmup > 0:
+        m.run(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.run(args.steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dev_ms, launches = m.last_run_stats()
+    if not np.isfinite(m.get_vorticity_field()).all():
+        raise SystemExit("c3p: vorticity is not finite after the timed run")
+    w = 8 if conf["fp64"] else 4
+    step_bytes = bvort_words_per_cell(method, W, H) * w * W * H
+    step_ms = dev_ms / args.steps
+    achieved = step_bytes / (step_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC, "value": W * H * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64" if conf["fp64"] else "f32",
+        "data": "synthetic (two Rossby modes), inputs resident in HBM",
+        "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": 1,
+                   "integrator": args.method, "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "whole step (hipFFT R2C/C2R + spectral scale + bv_stage_kernel)",
+                     "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
+                     "note": "device time of the run (hipEvents on the model's stream) per step; "
+                             "bytes = bvort_words_per_cell x cells"},
+        "launches_per_step": launches / args.steps,
+    }
+    if not args.no_cpu_baseline:
+        # the NumPy oracle (a port: no reference exists for this model), bounded sample
+        z = z0.astype(np.float64)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 15.0 and n < 50:
+            z = bo.step(z, cfg.dt, 1.0, 1.0, cfg.beta, cfg.viscosity, method)
+            n += 1
+        secs = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": W * H * n / secs, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+                                  "sample": f"oracle/bvort_oracle.py (NumPy, fp64): {W}x{H}, {n} steps, {secs:.2f} s"}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +250,8 @@ def main():
 
     conf = CONFIGS[args.config]
     method = METHODS[args.method]
+    if args.config == "c3p":
+        return bench_bvort(args, conf, method, world)
     cfg = ws.SimulationConfig()
     cfg.grid_width, cfg.grid_height, cfg.num_levels = conf["W"], conf["H"], conf["L"]
     cfg.model = conf["model"]
