@@ -85,24 +85,29 @@ template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 // DPP variant: independent 64-lane waves, horizontal neighbours by DPP lane shifts.
 constexpr int kDppCols = 64;
-// dma: y rows staged through LDS by LDS-DMA (16 B per lane) instead of VGPR loads
+// y rows: loaded into a VGPR ring (kDppVgpr), staged through LDS by LDS-DMA (16 B per lane)
+// and copied to the VGPR ring (kDppDma), or LDS-DMA staged and read from LDS in place
+// (kDppLdsY: fewer VGPRs, three waves per SIMD)
+enum DppMode : int { kDppVgpr = 0, kDppDma = 1, kDppLdsY = 2 };
 template <typename T>
-hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, bool dma);
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int mode);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone;
 // the x2 variant rounds it up to whole column pairs). The output window of strip s is
 // [s * out_w, (s + 1) * out_w); out_w is at most columns - 2 * margin, and when `aligned`
 // it is rounded down to whole 128-byte lines so no two strips write parts of one line.
-enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3 };
+enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3, kFusedDppLdsY = 4 };
 inline int fused_strip_cols(int variant) {
-    return variant == kFusedX2 ? 128 : (variant == kFusedDpp || variant == kFusedDppDma) ? 64 : 256;
+    return variant == kFusedX2 ? 128
+           : (variant == kFusedDpp || variant == kFusedDppDma || variant == kFusedDppLdsY) ? 64
+                                                                                             : 256;
 }
 // (the DMA variant rounds it up to whole 16-byte chunks: a strip's LDS-DMA chunks then
 // never straddle column 0, where a partly negative chunk would be dropped whole by the
 // buffer range check)
 inline int fused_margin(int variant, int nstages, int elem_bytes) {
     if (variant == kFusedX2) return (nstages + 1) / 2 * 2;
-    if (variant == kFusedDppDma) {
+    if (variant == kFusedDppDma || variant == kFusedDppLdsY) {
         const int g = 16 / elem_bytes;
         return (nstages + g - 1) / g * g;
     }

@@ -67,23 +67,34 @@ constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 
 // order LDS reads after LDS-DMA writes, so the kernel waits itself: every body issues
 // exactly 3 stores and every kG-th body 3 DMAs, hence a fixed count of younger vector-
 // memory ops at each wait (kWaitN below).
+// PF < 0 ("LDS-resident y"): as PF == 0, but the y rows stay in the LDS ring and each body
+// reads the three it needs for stage 1 (rows R-2, R-1, R) straight from it; only rows R-3
+// and R-4 (for the late stage updates) are kept in VGPRs. The ring is shorter (the DMA runs
+// one group ahead) and the VGPR ring of y rows is gone, which is what lets the kernel fit
+// three waves per SIMD (<= 168 VGPRs) where the others fit two.
 template <typename T, int NST, int POW2, int PF>
 __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
-    constexpr bool kDma = PF == 0;
+    constexpr bool kDma = PF <= 0;
+    constexpr bool kLdsY = PF < 0;
     constexpr int kG = 16 / (int)sizeof(T);                    // rows per DMA instruction
-    constexpr int kNR = (int)sizeof(T) == 8 ? 8 : 16;          // LDS ring rows
-    constexpr int kD = kDma ? ((int)sizeof(T) == 8 ? 6 : 8) : 0;  // DMA rows in flight
+    // LDS ring rows; DMA rows in flight
+    constexpr int kNR = kLdsY ? ((int)sizeof(T) == 8 ? 6 : 12) : ((int)sizeof(T) == 8 ? 8 : 16);
+    constexpr int kD = !kDma ? 0 : kLdsY ? kG : ((int)sizeof(T) == 8 ? 6 : 8);
     constexpr int kPf = kDma ? 0 : PF;
     constexpr int kU = kDma ? kNR : unroll_for(PF);            // DMA: ring slot == y ring index
     constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
     static_assert(kDma || kYb + kPf <= kU, "y ring too short");
     // a group's DMA may overwrite only slots whose rows were consumed (compiler lgkmcnt wait) in
-    // an earlier body: kNR >= kD + kG
-    static_assert(!kDma || (kU % kG == 0 && kU > kG + 4 && kNR >= kD + kG && kD % kG == 0), "DMA ring");
+    // an earlier body: kNR >= kD + kG (VGPR copy one body ahead) / kD + kG + 2 (LDS-resident
+    // rows R-2 .. R read in the body itself)
+    static_assert(!kDma || (kU % kG == 0 && kU % 2 == 0 && kNR >= kD + kG + (kLdsY ? 2 : 0) && kD % kG == 0 &&
+                            (kLdsY || kU > kG + 4)),
+                  "DMA ring");
     // younger vector-memory ops than a group's DMAs when that group is read: the stores of
-    // the kD - 1 bodies from its issue on, and the DMAs issued in between
-    constexpr int kWaitN = 3 * (kD - 1) + 3 * ((kD - 1) / (kG > 0 ? kG : 1));
+    // the bodies from its issue on (kD - 1 of them when read one body early into VGPRs, kD
+    // when read in place), and the DMAs issued in between (including the reading body's own)
+    constexpr int kWaitN = kLdsY ? 3 * kD + 3 * (kD / kG) : 3 * (kD - 1) + 3 * ((kD - 1) / (kG > 0 ? kG : 1));
 
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
@@ -168,11 +179,11 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     };
 
     const V3<T> Z{T(0), T(0), T(0)};
-    V3<T> Y[kU];                 // Y[r % kU] = y row r
+    V3<T> Y[kLdsY ? 2 : kU];     // Y[r % kU] = y row r (LDS-resident y: Y[r % 2] = row r, r <= R-3)
     V3<T> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
     V3<T> K2[2], K3[2];          // RK4 stage-2 / stage-3 tendencies at row r
 #pragma unroll
-    for (int i = 0; i < kU; ++i) Y[i] = Z;
+    for (int i = 0; i < (kLdsY ? 2 : kU); ++i) Y[i] = Z;
 #pragma unroll
     for (int i = 0; i < 2; ++i) S1[i] = S2[i] = S3[i] = K2[i] = K3[i] = Z;
 
@@ -188,7 +199,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
                 constexpr int v = Vs - kD;  // -kD .. -1
                 if constexpr (((v % kG) + kG) % kG == 0) dma(R0 + v + kD, v + kD);
                 store_row(y0 - 1, Z);
-                if constexpr (v == -1) {
+                if constexpr (v == -1 && !kLdsY) {
                     __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
 #pragma unroll
                     for (int k = 0; k < kG; ++k) Y[k] = read_row(k);
@@ -208,6 +219,9 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     // deep), so earlier bodies skip it -- NST(NST+1) stage-rows less per segment (RK4: 20).
     // A skipped final stage still issues its (dropped) store row, keeping every body's
     // load/store pattern identical for the compiler's vmcnt bookkeeping.
+    // y row R+d inside a body: LDS-resident rows R-2..R from this body's reads, older ones
+    // from the 2-row VGPR ring; otherwise the y VGPR ring
+#define YROW(d) (kLdsY ? ((d) == 0 ? yR0 : (d) == -1 ? yR1 : (d) == -2 ? yR2 : Y[r2(d)]) : Y[yi(d)])
     auto body = [&](auto Pc, auto Xc, auto Yc, auto Wc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
@@ -216,7 +230,18 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         constexpr auto on = [](int st) { return !WARM || P >= 2 * st; };
         constexpr auto yi = [](int d) { return ((P + d) % kU + kU) % kU; };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
-        if constexpr (kDma) {
+        constexpr auto sl = [](int d) { return ((P + d) % kNR + kNR) % kNR; };  // LDS ring slot of row R+d
+        V3<T> yR0, yR1, yR2;  // LDS-resident y: rows R, R-1, R-2
+        if constexpr (kLdsY) {
+            if constexpr (P % kG == 0) {
+                dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies
+                // rows R .. R+kG-1 (issued kD bodies ago) have landed
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
+            }
+            yR0 = read_row(sl(0));
+            yR1 = read_row(sl(-1));
+            yR2 = read_row(sl(-2));
+        } else if constexpr (kDma) {
             if constexpr (P % kG == 0) dma(R + kD, (P + kD) % kNR);  // slots of rows R+kD-kNR..: read
             if constexpr ((P + 1) % kG == 0) {  // rows R+1 .. R+kG: LDS -> y ring, needed from R+1 on
                 __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
@@ -232,36 +257,36 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         __builtin_amdgcn_sched_barrier(0);
 #endif
         if constexpr (WS_ABLATE == 2) {
-            store_row(R - NST, Y[yi(-NST)]);
+            store_row(R - NST, YROW(-NST));
             return;
         }
         if constexpr (!on(1)) {
             store_row(y0 - 1, Z);
             return;
         }
-        const V3<T> k1 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)], a.sp1,
+        const V3<T> k1 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 1, g, YROW(-2), YROW(-1), YROW(0), a.sp1,
                                                   a.gravity, a.coriolis_f);
         if constexpr (NST == 1) {
-            store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
+            store_row(R - 1, axpy(YROW(-1), a.c_dt, k1));  // Euler: y + dt k
         } else {
-            const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+            const V3<T> s1 = axpy(YROW(-1), a.c_half, k1);  // y + (0.5f dt) k
             if constexpr (on(2)) {
                 const V3<T> k2 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
                                                           a.gravity, a.coriolis_f);
                 if constexpr (NST == 2) {
-                    store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+                    store_row(R - 2, axpy(YROW(-2), a.c_dt, k2));  // RK2: y + dt k2
                 } else {
-                    const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                    const V3<T> s2 = axpy(YROW(-2), a.c_half, k2);
                     if constexpr (on(3)) {
                         const V3<T> k3 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2,
                                                                   a.sp2, a.gravity, a.coriolis_f);
-                        const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
+                        const V3<T> s3 = axpy(YROW(-3), a.c_dt, k3);
                         if constexpr (on(4)) {
                             const V3<T> k4 = stage_tend<POW2, XC, YC>(xlo, xhi, R - 4, g, S3[r2(-5)], S3[r2(-4)],
                                                                       s3, a.sp2, a.gravity, a.coriolis_f);
                             // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
                             const T two = T(2);
-                            const V3<T>& y4 = Y[yi(-4)];
+                            const V3<T> y4 = YROW(-4);
                             const V3<T>& kk2 = K2[r2(-4)];
                             const V3<T>& kk3 = K3[r2(-4)];
                             V3<T> o;
@@ -285,8 +310,12 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
             }
             S1[r2(-1)] = s1;  // after k2 read S1[r2(-3)] (same slot)
         }
+        // LDS-resident y: row R-2 becomes R-3 / R-4 of the next bodies (its slot held row
+        // R-4, read above)
+        if constexpr (kLdsY) Y[r2(-2)] = yR2;
     };
 
+#undef YROW
     auto march = [&](auto Xc, auto Yc) {
         auto period = [&](auto Wc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
@@ -312,8 +341,10 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
 }  // namespace
 
 template <typename T>
-hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, bool dma) {
+hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int mode) {
     const int out_w = a.out_w;
+    const bool dma = mode != kDppVgpr;
+    if (mode < kDppVgpr || mode > kDppLdsY) return hipErrorInvalidValue;
     if (out_w < 1 || out_w > kWave - 2 * fused_margin(dma ? kFusedDppDma : kFusedDpp, nstages, (int)sizeof(T)))
         return hipErrorInvalidValue;
     if (dma && out_w % (16 / (int)sizeof(T)) != 0) return hipErrorInvalidValue;  // chunk-aligned strips
@@ -329,8 +360,12 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     const dim3 grid((unsigned)nblocks), block(kWave);
     const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
 #define WS_DPP_GO(N, P2, PF) hipLaunchKernelGGL((fused_dpp_kernel<T, N, P2, PF>), grid, block, 0, s, a, g, nstrips, nsegs)
-#define WS_DPP_LAUNCH(N)                     \
-    if (dma) {                                  \
+#define WS_DPP_LAUNCH(N)                                          \
+    if (mode == kDppLdsY) {                                          \
+        if (sp_mode == kSpScaled) WS_DPP_GO(N, kSpScaled, -1);     \
+        else if (sp_mode == kSpMul) WS_DPP_GO(N, kSpMul, -1);      \
+        else WS_DPP_GO(N, kSpDiv, -1);                             \
+    } else if (dma) {                                            \
         if (sp_mode == kSpScaled) WS_DPP_GO(N, kSpScaled, 0);     \
         else if (sp_mode == kSpMul) WS_DPP_GO(N, kSpMul, 0);      \
         else WS_DPP_GO(N, kSpDiv, 0);                             \
@@ -350,7 +385,7 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
     return hipGetLastError();
 }
 
-template hipError_t launch_fused_step_dpp<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t, bool);
-template hipError_t launch_fused_step_dpp<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t, bool);
+template hipError_t launch_fused_step_dpp<float>(int, const FusedArgs<float>&, const Geom&, hipStream_t, int);
+template hipError_t launch_fused_step_dpp<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int);
 
 }  // namespace ws
