@@ -271,7 +271,8 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
 /* The fused step-kernel variant in use: kernel 0 = LDS workgroups, 1 = DPP waves (64
  * columns per wave), 2 = column pairs (128 columns per wave), 3 = DPP waves with y rows
  * staged through LDS by LDS-DMA, 4 = the same with y rows read from LDS in place (three
- * waves per SIMD), -1 = per-stage kernels;
+ * waves per SIMD), 5 = column pairs with y rows read from LDS in place, -1 = per-stage
+ * kernels;
  * seg_rows = output rows per segment, out_cols = output columns per strip (a multiple of
  * the 128-byte line when the strips are line-aligned). Chosen by timing every variant on
  * the real grid at the first run (all are bit-identical), unless WS_KERNEL / WS_SEG_ROWS /

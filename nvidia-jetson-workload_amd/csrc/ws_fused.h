@@ -96,9 +96,10 @@ hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom&
 // the x2 variant rounds it up to whole column pairs). The output window of strip s is
 // [s * out_w, (s + 1) * out_w); out_w is at most columns - 2 * margin, and when `aligned`
 // it is rounded down to whole 128-byte lines so no two strips write parts of one line.
-enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3, kFusedDppLdsY = 4 };
+enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3, kFusedDppLdsY = 4,
+                          kFusedX2Y = 5 };
 inline int fused_strip_cols(int variant) {
-    return variant == kFusedX2 ? 128
+    return variant == kFusedX2 || variant == kFusedX2Y ? 128
            : (variant == kFusedDpp || variant == kFusedDppDma || variant == kFusedDppLdsY) ? 64
                                                                                              : 256;
 }
@@ -107,7 +108,7 @@ inline int fused_strip_cols(int variant) {
 // buffer range check)
 inline int fused_margin(int variant, int nstages, int elem_bytes) {
     if (variant == kFusedX2) return (nstages + 1) / 2 * 2;
-    if (variant == kFusedDppDma || variant == kFusedDppLdsY) {
+    if (variant == kFusedDppDma || variant == kFusedDppLdsY || variant == kFusedX2Y) {
         const int g = 16 / elem_bytes;
         return (nstages + g - 1) / g * g;
     }
@@ -122,5 +123,8 @@ inline int fused_out_w(int variant, int nstages, int elem_bytes, bool aligned) {
 // x2 variant: independent 64-lane waves, two adjacent columns per lane (128-column strips).
 template <typename T>
 hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+// x2y variant: column pairs with y rows staged by LDS-DMA and read from LDS in place
+template <typename T>
+hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
 }  // namespace ws

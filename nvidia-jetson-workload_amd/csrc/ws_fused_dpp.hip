@@ -54,6 +54,12 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
 #ifndef WS_DPP_MINW
 #define WS_DPP_MINW 1
 #endif
+#ifndef WS_DPPY_MINW
+#define WS_DPPY_MINW 1  // LDS-resident y: 133 VGPRs (RK4 fp64) fit 3 waves per SIMD unforced
+#endif
+#ifndef WS_DPPY_GROUPS
+#define WS_DPPY_GROUPS 1  // LDS-resident y: DMA groups in flight (ring 6 rows fp64 / 12 fp32 at 1)
+#endif
 
 // s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
 // lgkmcnt[11:8], vmcnt[15:14]); the other counters at their maxima = not waited on
@@ -73,14 +79,15 @@ constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 
 // one group ahead) and the VGPR ring of y rows is gone, which is what lets the kernel fit
 // three waves per SIMD (<= 168 VGPRs) where the others fit two.
 template <typename T, int NST, int POW2, int PF>
-__global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
+__global__ __launch_bounds__(kWave, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
     constexpr bool kDma = PF <= 0;
     constexpr bool kLdsY = PF < 0;
     constexpr int kG = 16 / (int)sizeof(T);                    // rows per DMA instruction
-    // LDS ring rows; DMA rows in flight
-    constexpr int kNR = kLdsY ? ((int)sizeof(T) == 8 ? 6 : 12) : ((int)sizeof(T) == 8 ? 8 : 16);
-    constexpr int kD = !kDma ? 0 : kLdsY ? kG : ((int)sizeof(T) == 8 ? 6 : 8);
+    // DMA rows in flight; LDS ring rows (LDS-resident y: rows R-2 .. R+kD+kG-1, rounded up
+    // to whole groups)
+    constexpr int kD = !kDma ? 0 : kLdsY ? kG * WS_DPPY_GROUPS : ((int)sizeof(T) == 8 ? 6 : 8);
+    constexpr int kNR = kLdsY ? (kD + kG + 2 + kG - 1) / kG * kG : ((int)sizeof(T) == 8 ? 8 : 16);
     constexpr int kPf = kDma ? 0 : PF;
     constexpr int kU = kDma ? kNR : unroll_for(PF);            // DMA: ring slot == y ring index
     constexpr int kYb = NST + 1 < 3 ? 3 : NST + 1;  // past y rows used: R-kYb+1 .. R
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
     // load/store pattern identical for the compiler's vmcnt bookkeeping.
     // y row R+d inside a body: LDS-resident rows R-2..R from this body's reads, older ones
     // from the 2-row VGPR ring; otherwise the y VGPR ring
-#define YROW(d) (kLdsY ? ((d) == 0 ? yR0 : (d) == -1 ? yR1 : (d) == -2 ? yR2 : Y[r2(d)]) : Y[yi(d)])
+#define YROW(d) yrow.template operator()<d>()
     auto body = [&](auto Pc, auto Xc, auto Yc, auto Wc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
@@ -232,6 +239,13 @@ __global__ __launch_bounds__(kWave, WS_DPP_MINW) void fused_dpp_kernel(FusedArgs
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         constexpr auto sl = [](int d) { return ((P + d) % kNR + kNR) % kNR; };  // LDS ring slot of row R+d
         V3<T> yR0, yR1, yR2;  // LDS-resident y: rows R, R-1, R-2
+        const auto yrow = [&]<int d>() -> V3<T> {
+            if constexpr (!kLdsY) return Y[yi(d)];
+            else if constexpr (d == 0) return yR0;
+            else if constexpr (d == -1) return yR1;
+            else if constexpr (d == -2) return yR2;
+            else return Y[r2(d)];
+        };
         if constexpr (kLdsY) {
             if constexpr (P % kG == 0) {
                 dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies

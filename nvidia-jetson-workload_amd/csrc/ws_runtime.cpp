@@ -212,7 +212,7 @@ void convert(Dst* d, const Src* s, size_t n) {
 // simulation
 // ------------------------------------------------------------------------------------
 enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDpp = ws::kFusedDpp, kKernX2 = ws::kFusedX2,
-                         kKernDppDma = ws::kFusedDppDma, kKernDppLdsY = ws::kFusedDppLdsY };
+                         kKernDppDma = ws::kFusedDppDma, kKernDppLdsY = ws::kFusedDppLdsY, kKernX2Y = ws::kFusedX2Y };
 
 struct ws_sim {
     ws_config_t cfg{};
@@ -272,7 +272,7 @@ struct ws_sim {
     // warm-up rows stay a small overhead. The autotuner also tries other counts.
     int32_t seg_rows(int nst) const {
         if (seg_override > 0) return seg_override;
-        int64_t want_blocks = kernel == kKernX2 ? 2048 : (kernel == kKernDpp || kernel == kKernDppDma || kernel == kKernDppLdsY) ? 4096 : 512;
+        int64_t want_blocks = kernel == kKernX2 || kernel == kKernX2Y ? 2048 : (kernel == kKernDpp || kernel == kKernDppDma || kernel == kKernDppLdsY) ? 4096 : 512;
         if (want_blocks_override > 0) want_blocks = want_blocks_override;
         return seg_for_blocks(nst, want_blocks, 24 * nst);
     }
@@ -370,6 +370,7 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     const ws::Geom g = c->geom();
     switch (s->kernel) {
         case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
+        case kKernX2Y: WS_HIP_CHECK(ws::launch_fused_step_x2y<T>(nst, a, g, st)); break;
         case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppVgpr)); break;
         case kKernDppDma: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppDma)); break;
         case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppLdsY)); break;
@@ -490,7 +491,7 @@ void autotune(ws_sim* s) {
     };
     std::vector<Cand> cands;
     const int fixed_seg = s->seg_override;
-    for (int k : {kKernDpp, kKernDppDma, kKernDppLdsY, kKernX2, kKernLds}) {
+    for (int k : {kKernDpp, kKernDppDma, kKernDppLdsY, kKernX2, kKernX2Y, kKernLds}) {
         for (bool al : {false, true}) {
             if (s->align_fixed && al != s->align) continue;
             s->kernel = k;
@@ -513,7 +514,7 @@ void autotune(ws_sim* s) {
                 const int wave_per_block = k == kKernLds ? 4 : 1;
                 for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
                     segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
-                if (k == kKernDppLdsY)  // three to four waves per SIMD fit: shorter segments pay
+                if (k == kKernDppLdsY || k == kKernX2Y)  // more waves per SIMD fit: shorter segments pay
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
@@ -680,6 +681,7 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
                         : std::strcmp(e, "dpp") == 0    ? kKernDpp
                         : std::strcmp(e, "dppdma") == 0 ? kKernDppDma
                         : std::strcmp(e, "dppy") == 0   ? kKernDppLdsY
+                        : std::strcmp(e, "x2y") == 0    ? kKernX2Y
                                                         : kKernX2;
             s->kernel_fixed = true;
         }

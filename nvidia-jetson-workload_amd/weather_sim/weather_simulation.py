@@ -676,7 +676,7 @@ class WeatherSimulation:
         k, seg, cols = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg), ctypes.byref(cols)))
         return ({-1: "stage_kernels", 0: "fused_lds", 1: "fused_dpp", 2: "fused_x2", 3: "fused_dppdma",
-                 4: "fused_dppy"}[k.value], seg.value,
+                 4: "fused_dppy", 5: "fused_x2y"}[k.value], seg.value,
                 cols.value)
 
     def comm_allreduce_max(self, value):

@@ -56,8 +56,8 @@ def load(sim, s0):
     g.set_humidity_field(s0["q"])
 
 
-KERNELS = [("1", "x2"), ("1", "dpp"), ("1", "dppdma"), ("1", "dppy"), ("1", "lds"), ("0", "x2")]
-KERNEL_IDS = ["fused_x2", "fused_dpp", "fused_dppdma", "fused_dppy", "fused_lds", "stage_kernels"]
+KERNELS = [("1", "x2"), ("1", "dpp"), ("1", "dppdma"), ("1", "dppy"), ("1", "x2y"), ("1", "lds"), ("0", "x2")]
+KERNEL_IDS = ["fused_x2", "fused_dpp", "fused_dppdma", "fused_dppy", "fused_x2y", "fused_lds", "stage_kernels"]
 
 
 @pytest.mark.parametrize("fused,kernel", KERNELS, ids=KERNEL_IDS)
@@ -272,7 +272,7 @@ def test_pe_levels_match_reference_per_level():
             assert _digest(got[f]) == h, (k, f)
 
 
-@pytest.mark.parametrize("kernel", ["x2", "dpp", "dppdma", "dppy", "lds"])
+@pytest.mark.parametrize("kernel", ["x2", "dpp", "dppdma", "dppy", "x2y", "lds"])
 @pytest.mark.parametrize("seg_rows", ["0", "5", "33"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
@@ -322,7 +322,7 @@ def test_fused_non_pow2_spacing_vs_oracle():
         np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
 
 
-@pytest.mark.parametrize("kernel,seg_rows", [("x2", "0"), ("x2", "6"), ("dpp", "6"), ("dppdma", "6"), ("dppy", "6"), ("dppy", "0"), ("lds", "6")])
+@pytest.mark.parametrize("kernel,seg_rows", [("x2", "0"), ("x2", "6"), ("dpp", "6"), ("dppdma", "6"), ("dppy", "6"), ("dppy", "0"), ("x2y", "6"), ("x2y", "0"), ("lds", "6")])
 @pytest.mark.parametrize("nslabs", [2, 3, 5])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])

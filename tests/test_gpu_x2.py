@@ -52,7 +52,7 @@ def test_x2_non_pow2(method, monkeypatch):
 
 
 @pytest.mark.parametrize("W", [61, 300, 700])
-@pytest.mark.parametrize("kernel", ["dpp", "dppdma", "dppy", "x2", "lds"])
+@pytest.mark.parametrize("kernel", ["dpp", "dppdma", "dppy", "x2", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_line_aligned_strips(W, kernel, method, fp64, monkeypatch):

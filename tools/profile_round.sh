@@ -12,13 +12,13 @@ timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS 
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
 read KERN KNAME SEG ALIGN < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
-k={'fused_dpp':'dpp','fused_dppdma':'dppdma','fused_dppy':'dppy','fused_x2':'x2','fused_lds':'lds'}.get(d['kernel'],'dpp')
-n={'dpp':'fused_dpp_kernel','dppdma':'fused_dpp_kernel','dppy':'fused_dpp_kernel','x2':'fused_x2_kernel','lds':'fused_step_kernel'}[k]
+k={'fused_dpp':'dpp','fused_dppdma':'dppdma','fused_dppy':'dppy','fused_x2':'x2','fused_x2y':'x2y','fused_lds':'lds'}.get(d['kernel'],'dpp')
+n={'dpp':'fused_dpp_kernel','dppdma':'fused_dpp_kernel','dppy':'fused_dpp_kernel','x2y':'fused_x2y_kernel','x2':'fused_x2_kernel','lds':'fused_step_kernel'}[k]
 nst={'euler':1,'rk2':2,'rk4':4}['$METHOD']
 nst=2 if nst==4 and '$CFG' in ('c3','c4') else nst
 g=16//(8 if '$CFG' in ('c2','c5') or '$CFG'.startswith('c2_') else 4)
-margin=(nst+1)//2*2 if k=='x2' else ((nst+g-1)//g*g if k in ('dppdma','dppy') else nst)
-full={'dpp':64,'dppdma':64,'dppy':64,'x2':128,'lds':256}[k]-2*margin
+margin=(nst+1)//2*2 if k=='x2' else ((nst+g-1)//g*g if k in ('dppdma','dppy','x2y') else nst)
+full={'dpp':64,'dppdma':64,'dppy':64,'x2':128,'x2y':128,'lds':256}[k]-2*margin
 print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0)")
 echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN"
 export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN
