@@ -56,6 +56,11 @@ CONFIGS = {
     "c3p": dict(W=2048, H=2048, L=1, model=1, fp64=False, ic="rossby",
                 workload="C3 physics mode: barotropic vorticity (Arakawa Jacobian + Laplacian, hipFFT Poisson) "
                          "2048x2048 fp32"),
+    # C4 as BASELINE describes it ("3D stencil, vertical columns in LDS"): the physics-mode
+    # layered primitive-equation model (no reference semantics)
+    "c4p": dict(W=1024, H=1024, L=32, model=2, fp64=False, ic="layers",
+                workload="C4 physics mode: layered primitive equations (isopycnal, Montgomery-potential column "
+                         "scan in LDS) 1024x1024x32 fp32"),
 }
 METHODS = {"euler": 0, "rk2": 1, "rk4": 2}
 
@@ -222,6 +227,91 @@ def bench_bvort(args, conf, method, world):
     print(json.dumps(result), flush=True)
 
 
+def lpe_words_per_cell(method):
+    """Algorithmic traffic of one layered-PE step in words per cell and level: per stage
+    the stage input u, v, h, h again for the column scan, the step's base u, v, h, the RK4
+    accumulator (read from stage 2 on, written up to stage 3) and the stage output."""
+    stages = {0: [(0, 0)], 1: [(0, 0), (0, 0)], 2: [(0, 3), (3, 3), (3, 3), (3, 0)]}[method]
+    return sum(3 + 1 + 3 + acc_r + acc_w + 3 for acc_r, acc_w in stages)
+
+
+def bench_lpe(args, conf, method, world):
+    """Physics-mode layered primitive equations (config c4p), one GPU."""
+    import numpy as np
+    import torch
+    import weather_sim as ws
+    from oracle import layered_pe_oracle as lp
+
+    if world > 1:
+        raise SystemExit("c4p runs on one GPU")
+    W, H, L = conf["W"], conf["H"], conf["L"]
+    cfg = ws.SimulationConfig()
+    cfg.grid_width, cfg.grid_height, cfg.num_levels = W, H, L
+    cfg.integration_method = method
+    cfg.double_precision = conf["fp64"]
+    cfg.dx = cfg.dy = 1000.0
+    cfg.dt, cfg.gravity, cfg.coriolis_f = 5.0, 9.81, 1e-4
+    gp = 0.02
+    m = ws.LayeredPrimitiveEquationsModel(cfg, reduced_gravity=gp)
+
+    def initial(Wi, Hi):
+        u, v, h = lp.rest_state(L, Hi, Wi, [40.0 + 2.0 * k for k in range(L)])
+        x = np.arange(Wi)[None, :]
+        y = np.arange(Hi)[:, None]
+        for k in range(L):
+            h[k] += 0.5 * np.cos(2 * np.pi * (3 * x / Wi + 2 * y / Hi) + 0.1 * k)
+        return u, v, h
+
+    s0 = initial(W, H)
+    m.set_state(*s0)
+    if args.warmup > 0:
+        m.run(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.run(args.steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dev_ms, launches = m.last_run_stats()
+    if not np.isfinite(m.get_field("h")).all():
+        raise SystemExit("c4p: state is not finite after the timed run")
+    w = 8 if conf["fp64"] else 4
+    cells = W * H * L
+    step_bytes = lpe_words_per_cell(method) * w * cells
+    step_ms = dev_ms / args.steps
+    achieved = step_bytes / (step_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC, "value": cells * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64" if conf["fp64"] else "f32",
+        "data": "synthetic (stacked layers with an interface wave), inputs resident in HBM",
+        "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": L,
+                   "integrator": args.method, "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "lpe_stage_kernel (whole step)",
+                     "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
+                     "note": "device time of the run (hipEvents on the model's stream) per step; "
+                             "bytes = lpe_words_per_cell x cells x levels"},
+        "launches_per_step": launches / args.steps,
+    }
+    if not args.no_cpu_baseline:
+        # the NumPy oracle (a port: no reference exists for this model) on a 256 x 256 x L
+        # sample of the same per-cell work, bounded
+        Ws = Hs = 256
+        s = initial(Ws, Hs)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 15.0 and n < 50:
+            s = lp.step(s, cfg.dt, cfg.dx, cfg.dy, cfg.gravity, gp, cfg.coriolis_f, method)
+            n += 1
+        secs = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": Ws * Hs * L * n / secs, "unit": "cell-updates/s", "cores": 1,
+                                  "kind": "port",
+                                  "sample": f"oracle/layered_pe_oracle.py (NumPy, fp64): {Ws}x{Hs}x{L}, {n} steps, "
+                                            f"{secs:.2f} s"}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,6 +342,8 @@ def main():
     method = METHODS[args.method]
     if args.config == "c3p":
         return bench_bvort(args, conf, method, world)
+    if args.config == "c4p":
+        return bench_lpe(args, conf, method, world)
     cfg = ws.SimulationConfig()
     cfg.grid_width, cfg.grid_height, cfg.num_levels = conf["W"], conf["H"], conf["L"]
     cfg.model = conf["model"]

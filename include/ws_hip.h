@@ -254,6 +254,27 @@ int ws_bvort_run(ws_bvort_t* model, int32_t num_steps);
 int ws_bvort_get_state(const ws_bvort_t* model, double* time, int32_t* step, double* last_run_ms,
                        int64_t* last_run_launches);
 
+/* ---- physics-mode layered primitive-equation model (new) ----------- */
+/* BASELINE config C4 names a 3-D primitive-equation stencil with vertical columns; the
+ * reference has none (its PE model runs the SWE tendencies level by level, which ws_sim_*
+ * reproduces bit for bit). This is that model, defined by oracle/layered_pe_oracle.py:
+ * hydrostatic primitive equations in isopycnal coordinates -- num_levels stacked layers of
+ * constant density (k = 0 on top), flat bottom, doubly periodic -- coupled through the
+ * Montgomery potential M_0 = g eta_0, M_k = M_{k-1} + reduced_gravity * eta_k (eta_k = height
+ * of layer k's top). From cfg it reads grid_width/height, num_levels, dx, dy, dt, gravity,
+ * coriolis_f, integration_method (Euler / RK2 / classical RK4), double_precision and
+ * device_id. Fields are (num_levels, height, width) arrays: 0 u, 1 v, 2 h (thickness). */
+typedef struct ws_lpe ws_lpe_t;
+int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out);
+int ws_lpe_destroy(ws_lpe_t* model);
+int ws_lpe_set_field(ws_lpe_t* model, int32_t field, const void* host, int32_t levels, int32_t height,
+                     int32_t width, int32_t dtype);
+int ws_lpe_get_field(ws_lpe_t* model, int32_t field, void* host, int32_t levels, int32_t height, int32_t width,
+                     int32_t dtype);
+int ws_lpe_run(ws_lpe_t* model, int32_t num_steps);
+int ws_lpe_get_state(const ws_lpe_t* model, double* time, int32_t* step, double* last_run_ms,
+                     int64_t* last_run_launches);
+
 /* ---- per-kernel timing (measurement) --------------------------------------------- */
 /* When enabled, ws_sim_run / ws_sim_step time their kernels with hipEvents on the
  * simulation's stream: a run whose steps are one fused launch each (and nothing else on

@@ -14,7 +14,7 @@ from .weather_simulation import (  # noqa: F401
     RandomInitialCondition, SimulationConfig, SimulationModel, UniformInitialCondition, VortexInitialCondition,
     WeatherGrid, WeatherSimulation, WeatherSimulationWrapper, ZonalFlowInitialCondition, create_initial_condition,
     get_available_initial_conditions, get_device_info, is_cuda_available, register_all_initial_conditions)
-from .physics import BarotropicVorticityModel  # noqa: F401
+from .physics import BarotropicVorticityModel, LayeredPrimitiveEquationsModel  # noqa: F401
 from .output import (  # noqa: F401
     CSVOutputManager, Snapshot, proto_classes, read_csv, weather_sim_result, weather_sim_update, write_csv)
 

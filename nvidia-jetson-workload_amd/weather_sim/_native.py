@@ -122,6 +122,12 @@ SIGNATURES = {
     "ws_bvort_get_field": [_P, _I, _P, _I, _I, _I],
     "ws_bvort_run": [_P, _I],
     "ws_bvort_get_state": [_P, _PD, _PI, _PD, _PL],
+    "ws_lpe_create": [ctypes.POINTER(ws_config_t), _D, _PP],
+    "ws_lpe_destroy": [_P],
+    "ws_lpe_set_field": [_P, _I, _P, _I, _I, _I, _I],
+    "ws_lpe_get_field": [_P, _I, _P, _I, _I, _I, _I],
+    "ws_lpe_run": [_P, _I],
+    "ws_lpe_get_state": [_P, _PD, _PI, _PD, _PL],
 }
 _RESTYPES = {"ws_last_error": ctypes.c_char_p, "ws_config_default": None}
 

@@ -108,3 +108,92 @@ class BarotropicVorticityModel:
 
     def enstrophy(self):
         return 0.5 * float(np.sum(self.get_vorticity_field().astype(np.float64) ** 2))
+
+
+_LPE_FIELDS = {"u": 0, "v": 1, "h": 2}
+
+
+class LayeredPrimitiveEquationsModel:
+    """Physics-mode primitive equations: `config.num_levels` stacked
+    constant-density layers (k = 0 on top) over a flat bottom, doubly periodic, coupled by
+    hydrostatic balance through the Montgomery potential
+
+        M_0 = g * eta_0,  M_k = M_{k-1} + g' * eta_k     (eta_k = sum_{j >= k} h_j)
+        du/dt = -u u_x - v u_y - M_x + f v,  dv/dt = -u v_x - v v_y - M_y - f u,
+        dh/dt = -(h u)_x - (h v)_y
+
+    -- the "3D stencil, vertical columns" model BASELINE's C4 describes, which the reference
+    never implemented (its PrimitiveEquations model steps each level with the SWE tendencies,
+    weather_simulation.cpp:542-560; `WeatherSimulation` reproduces that bit for bit). Defined
+    by oracle/layered_pe_oracle.py; g = config.gravity, f = config.coriolis_f,
+    g' = `reduced_gravity`. Fields are (levels, height, width) arrays; h is layer thickness.
+    """
+
+    def __init__(self, config, reduced_gravity=0.05):
+        from .weather_simulation import SimulationConfig
+        if not isinstance(config, SimulationConfig):
+            raise TypeError("LayeredPrimitiveEquationsModel expects a SimulationConfig")
+        raw = config._to_c()
+        h = ctypes.c_void_p()
+        check(lib.ws_lpe_create(ctypes.byref(raw), float(reduced_gravity), ctypes.byref(h)))
+        self._h = h
+        self.levels = int(config.num_levels)
+        self.width, self.height = int(config.grid_width), int(config.grid_height)
+        self.dtype = np.float64 if config.double_precision else np.float32
+        self.reduced_gravity = float(reduced_gravity)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.ws_lpe_destroy(h)
+            self._h = None
+
+    def _shape(self):
+        return (self.levels, self.height, self.width)
+
+    def set_field(self, name, arr):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=self.dtype))
+        if a.shape != self._shape():
+            raise RuntimeError(f"{name}: expected shape {self._shape()}, got {a.shape}")
+        code = WS_F64 if self.dtype == np.float64 else WS_F32
+        check(lib.ws_lpe_set_field(self._h, _LPE_FIELDS[name], a.ctypes.data_as(ctypes.c_void_p), *a.shape, code))
+
+    def get_field(self, name):
+        out = np.empty(self._shape(), dtype=self.dtype)
+        code = WS_F64 if self.dtype == np.float64 else WS_F32
+        check(lib.ws_lpe_get_field(self._h, _LPE_FIELDS[name], out.ctypes.data_as(ctypes.c_void_p), *out.shape, code))
+        return out
+
+    def set_state(self, u, v, h):
+        for name, a in (("u", u), ("v", v), ("h", h)):
+            self.set_field(name, a)
+
+    def get_state(self):
+        return self.get_field("u"), self.get_field("v"), self.get_field("h")
+
+    def step(self):
+        self.run(1)
+
+    def run(self, num_steps):
+        check(lib.ws_lpe_run(self._h, int(num_steps)))
+        return int(num_steps)
+
+    def _st(self):
+        t, s, ms, n = ctypes.c_double(), ctypes.c_int32(), ctypes.c_double(), ctypes.c_int64()
+        check(lib.ws_lpe_get_state(self._h, ctypes.byref(t), ctypes.byref(s), ctypes.byref(ms), ctypes.byref(n)))
+        return t.value, s.value, ms.value, n.value
+
+    def get_current_time(self):
+        return self._st()[0]
+
+    def get_current_step(self):
+        return self._st()[1]
+
+    def last_run_stats(self):
+        """(device ms of the last run(), kernel launches it made)"""
+        _, _, ms, n = self._st()
+        return ms, n
+
+    def layer_mass(self):
+        """sum of h over each layer (conserved exactly by the flux-form continuity equation)"""
+        return self.get_field("h").astype(np.float64).sum(axis=(1, 2))

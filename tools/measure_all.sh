@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/all
 mkdir -p $OUT
-for spec in ${SPECS:-"c2 rk4" "c2 rk2" "c2 euler" "c3 rk4" "c4 rk4" "c5 rk4" "c2_slab2 rk4" "c2_slab4 rk4" "c2_slab8 rk4" "c3p rk4"}; do
+for spec in ${SPECS:-"c2 rk4" "c2 rk2" "c2 euler" "c3 rk4" "c4 rk4" "c5 rk4" "c2_slab2 rk4" "c2_slab4 rk4" "c2_slab8 rk4" "c3p rk4" "c4p rk4"}; do
   set -- $spec
   timeout -k 10 300 python bench.py --config $1 --method $2 --steps ${STEPS:-200} --warmup ${WARM:-300} \
       ${CPU:---no-cpu-baseline} > $OUT/$1_$2.json 2> $OUT/$1_$2.err
