@@ -91,6 +91,13 @@ constexpr int kDppCols = 64;
 enum DppMode : int { kDppVgpr = 0, kDppDma = 1, kDppLdsY = 2 };
 template <typename T>
 hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int mode);
+// the three modes' launchers (one translation unit each)
+template <typename T>
+hipError_t launch_dpp_vgpr(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+template <typename T>
+hipError_t launch_dpp_dma(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+template <typename T>
+hipError_t launch_dpp_ldsy(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone;
 // the x2 variant rounds it up to whole column pairs). The output window of strip s is

@@ -1,6 +1,8 @@
 #!/bin/bash
-# Build an A/B measurement variant of libws_hip.so with extra -D flags on the DPP kernel:
-#   tools/variant.sh NAME "-DWS_DPP_PF=5 ..."   -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
+# Build an A/B measurement variant of libws_hip.so with extra -D flags on one kernel file
+# (default ws_fused_dpp.hip = the DPP kernel's VGPR mode; ws_fused_dpp_dma.hip / _ldsy.hip
+# hold its other modes):
+#   tools/variant.sh NAME "-DWS_DPP_PF=5 ..." [file]  -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
 set -eu
 cd "$(dirname "$0")/../nvidia-jetson-workload_amd/csrc"
 make -s -j8 >/dev/null
