@@ -246,6 +246,7 @@ struct ws_sim {
     int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
     bool align = false;       // strip output windows on whole 128-byte lines (WS_ALIGN fixes it)
     bool kernel_fixed = false, seg_fixed = false, align_fixed = false;
+    bool scaled = false;      // WS_SCALED=1: scaled tendencies (opt-in, ws_fused.h)
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
@@ -365,8 +366,7 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
     // opt-in scaled tendencies (ws_fused.h): not bit-exact in the subnormal range
-    static const bool scaled_ok = env_int("WS_SCALED", 0) != 0;
-    if (scaled_ok) ws::scale_tendencies(a);
+    if (s->scaled) ws::scale_tendencies(a);
     const ws::Geom g = c->geom();
     switch (s->kernel) {
         case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
@@ -676,6 +676,7 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
+        s->scaled = env_int("WS_SCALED", 0) != 0;
         if (const char* e = std::getenv("WS_KERNEL")) {
             s->kernel = std::strcmp(e, "lds") == 0      ? kKernLds
                         : std::strcmp(e, "dpp") == 0    ? kKernDpp
