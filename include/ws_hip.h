@@ -263,7 +263,8 @@ int ws_bvort_get_state(const ws_bvort_t* model, double* time, int32_t* step, dou
  * Montgomery potential M_0 = g eta_0, M_k = M_{k-1} + reduced_gravity * eta_k (eta_k = height
  * of layer k's top). From cfg it reads grid_width/height, num_levels, dx, dy, dt, gravity,
  * coriolis_f, integration_method (Euler / RK2 / classical RK4), double_precision and
- * device_id. Fields are (num_levels, height, width) arrays: 0 u, 1 v, 2 h (thickness). */
+ * device_id; any number of levels. Fields are (num_levels, height, width) arrays: 0 u, 1 v,
+ * 2 h (thickness). */
 typedef struct ws_lpe ws_lpe_t;
 int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out);
 int ws_lpe_destroy(ws_lpe_t* model);

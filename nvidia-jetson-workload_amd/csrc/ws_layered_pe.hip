@@ -10,10 +10,10 @@
 //     dh/dt = -(h u)_x - (h v)_y
 //
 // One kernel per RK stage. A 32 x 8 tile of columns plus a 1-column halo computes the
-// Montgomery potential of every column by a vertical scan (the columns' whole M profiles
-// live in LDS: L x 10 x 34 values), then each thread walks its column level by level,
-// taking M's horizontal neighbours from LDS and u, v, h's from global memory (L1/L2), and
-// applies the stage update (and the RK4 accumulator) in the same pass.
+// Montgomery potential of every column by a vertical scan, chunk by chunk of levels (each
+// chunk's M profiles in LDS), and after each chunk every thread walks its own column through
+// those levels, taking M's horizontal neighbours from LDS and u, v, h's from global memory
+// (L1/L2), and applies the stage update (and the RK4 accumulator) in the same pass.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -43,81 +43,112 @@ struct LpeArgs {
 
 __device__ __forceinline__ int wrapi(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
+// Levels are processed in chunks of kChunk: the column scan's running state (total
+// thickness, prefix, M of the level above) stays in registers, each chunk's M profile goes
+// to LDS (kChunk x 10 x 34 values: 11 KB fp32), so many workgroups fit a CU and the
+// column walk of one chunk overlaps the other workgroups' loads.
+#ifndef WS_LPE_CHUNK
+#define WS_LPE_CHUNK 8
+#endif
+constexpr int kChunk = WS_LPE_CHUNK;
+#ifndef WS_LPE_UNROLL
+#define WS_LPE_UNROLL 2  // measured at 1024^2 x 32 fp32 RK4: 1 / 2 / 4 / 8 -> 15.2 / 16.2 / 14.2 / 15.5 Gcell/s
+#endif
+constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
+
 template <typename T>
 __global__ __launch_bounds__(kTX* kTY) void lpe_stage_kernel(LpeArgs<T> a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    T* Ms = (T*)lds_raw;  // [L][kCY][kCX]
+    __shared__ T Ms[kChunk][kCY][kCX];
     const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
     const int tid = threadIdx.y * kTX + threadIdx.x;
-    // phase 1: Montgomery potential of the tile's columns and their halo (oracle order:
-    // total = h_0 + h_1 + ...; eta_k = total - (h_0 + ... + h_{k-1}))
-    for (int c = tid; c < kCX * kCY; c += kTX * kTY) {
-        const int lx = c % kCX, ly = c / kCX;
+    // scan state of this thread's columns of the tile + halo (oracle order: total = h_0 +
+    // h_1 + ...; eta_k = total - (h_0 + ... + h_{k-1}); M_0 = g eta_0, M_k = M_{k-1} + g' eta_k)
+    const T* hc[kColsPerThread];
+    T total[kColsPerThread], prefix[kColsPerThread], Mprev[kColsPerThread];
+#pragma unroll
+    for (int i = 0; i < kColsPerThread; ++i) {
+        const int c = tid + i * kTX * kTY;
+        const int cc = c < kCX * kCY ? c : 0;
+        const int lx = cc % kCX, ly = cc / kCX;
         int gx = (x0 + lx - 1) % a.W;
         if (gx < 0) gx += a.W;
         int gy = (y0 + ly - 1) % a.H;
         if (gy < 0) gy += a.H;
-        const T* hc = a.h + (int64_t)gy * a.W + gx;
-        T total = T(0);
+        hc[i] = a.h + (int64_t)gy * a.W + gx;
+        T t = T(0);
+        if (c < kCX * kCY) {
 #pragma unroll 8
-        for (int k = 0; k < a.L; ++k) total = total + hc[(int64_t)k * a.lstride];
-        T prefix = T(0), M = T(0);
-        for (int k = 0; k < a.L; ++k) {
-            const T eta = total - prefix;
-            M = k == 0 ? a.g * eta : M + a.gp * eta;
-            Ms[(k * kCY + ly) * kCX + lx] = M;
-            prefix = prefix + hc[(int64_t)k * a.lstride];
+            for (int k = 0; k < a.L; ++k) t = t + hc[i][(int64_t)k * a.lstride];
         }
+        total[i] = t;
+        prefix[i] = T(0);
+        Mprev[i] = T(0);
     }
-    __syncthreads();
     const int x = x0 + threadIdx.x, y = y0 + threadIdx.y;
-    if (x >= a.W || y >= a.H) return;
+    const bool inside = x < a.W && y < a.H;
     const int lx = threadIdx.x + 1, ly = threadIdx.y + 1;
-    const int64_t oc = (int64_t)y * a.W + x;
-    const int64_t oe = (int64_t)y * a.W + wrapi(x + 1, a.W), ow = (int64_t)y * a.W + wrapi(x - 1, a.W);
-    const int64_t on = (int64_t)wrapi(y + 1, a.H) * a.W + x, os = (int64_t)wrapi(y - 1, a.H) * a.W + x;
-#ifndef WS_LPE_UNROLL
-#define WS_LPE_UNROLL 1  // measured: 1 beats 4 and 8 (c4p 13.5 vs 11.6 / 12.6 Gcell/s)
-#endif
+    const int xc = inside ? x : 0, yc = inside ? y : 0;
+    const int64_t oc = (int64_t)yc * a.W + xc;
+    const int64_t oe = (int64_t)yc * a.W + wrapi(xc + 1, a.W), ow = (int64_t)yc * a.W + wrapi(xc - 1, a.W);
+    const int64_t on = (int64_t)wrapi(yc + 1, a.H) * a.W + xc, os = (int64_t)wrapi(yc - 1, a.H) * a.W + xc;
+    for (int k0 = 0; k0 < a.L; k0 += kChunk) {
+        const int nk = a.L - k0 < kChunk ? a.L - k0 : kChunk;
+#pragma unroll
+        for (int i = 0; i < kColsPerThread; ++i) {
+            const int c = tid + i * kTX * kTY;
+            if (c >= kCX * kCY) continue;
+            const int lxc = c % kCX, lyc = c / kCX;
+            for (int j = 0; j < nk; ++j) {
+                const int k = k0 + j;
+                const T eta = total[i] - prefix[i];
+                Mprev[i] = k == 0 ? a.g * eta : Mprev[i] + a.gp * eta;
+                Ms[j][lyc][lxc] = Mprev[i];
+                prefix[i] = prefix[i] + hc[i][(int64_t)k * a.lstride];
+            }
+        }
+        __syncthreads();
+        if (inside) {
 #pragma unroll WS_LPE_UNROLL
-    for (int k = 0; k < a.L; ++k) {
-        const int64_t lo = (int64_t)k * a.lstride;
-        const T* U = a.u + lo;
-        const T* V = a.v + lo;
-        const T* Hh = a.h + lo;
-        const T u = U[oc], v = V[oc];
-        const T ue = U[oe], uw = U[ow], un = U[on], us = U[os];
-        const T ve = V[oe], vw = V[ow], vn = V[on], vs = V[os];
-        const T he = Hh[oe], hw = Hh[ow], hn = Hh[on], hs = Hh[os];
-        const T* Mk = Ms + k * kCY * kCX;
-        const T Me = Mk[ly * kCX + lx + 1], Mw = Mk[ly * kCX + lx - 1];
-        const T Mn = Mk[(ly + 1) * kCX + lx], Mso = Mk[(ly - 1) * kCX + lx];
-        const T u_x = (ue - uw) * a.ix, u_y = (un - us) * a.iy;
-        const T v_x = (ve - vw) * a.ix, v_y = (vn - vs) * a.iy;
-        const T M_x = (Me - Mw) * a.ix, M_y = (Mn - Mso) * a.iy;
-        const T du = -u * u_x - v * u_y - M_x + a.f * v;
-        const T dv = -u * v_x - v * v_y - M_y - a.f * u;
-        const T dh = -((he * ue - hw * uw) * a.ix) - (hn * vn - hs * vs) * a.iy;
-        const int64_t o = lo + oc;
-        const T b0 = a.bu[o], b1 = a.bv[o], b2 = a.bh[o];
-        if (a.acc_mode == 3) {
-            a.ou[o] = b0 + a.c * (a.au[o] + du);
-            a.ov[o] = b1 + a.c * (a.av[o] + dv);
-            a.oh[o] = b2 + a.c * (a.ah[o] + dh);
-            continue;
+            for (int j = 0; j < nk; ++j) {
+                const int64_t lo = (int64_t)(k0 + j) * a.lstride;
+                const T* U = a.u + lo;
+                const T* V = a.v + lo;
+                const T* Hh = a.h + lo;
+                const T u = U[oc], v = V[oc];
+                const T ue = U[oe], uw = U[ow], un = U[on], us = U[os];
+                const T ve = V[oe], vw = V[ow], vn = V[on], vs = V[os];
+                const T he = Hh[oe], hw = Hh[ow], hn = Hh[on], hs = Hh[os];
+                const T Me = Ms[j][ly][lx + 1], Mw = Ms[j][ly][lx - 1];
+                const T Mn = Ms[j][ly + 1][lx], Mso = Ms[j][ly - 1][lx];
+                const T u_x = (ue - uw) * a.ix, u_y = (un - us) * a.iy;
+                const T v_x = (ve - vw) * a.ix, v_y = (vn - vs) * a.iy;
+                const T M_x = (Me - Mw) * a.ix, M_y = (Mn - Mso) * a.iy;
+                const T du = -u * u_x - v * u_y - M_x + a.f * v;
+                const T dv = -u * v_x - v * v_y - M_y - a.f * u;
+                const T dh = -((he * ue - hw * uw) * a.ix) - (hn * vn - hs * vs) * a.iy;
+                const int64_t o = lo + oc;
+                const T b0 = a.bu[o], b1 = a.bv[o], b2 = a.bh[o];
+                if (a.acc_mode == 3) {
+                    a.ou[o] = b0 + a.c * (a.au[o] + du);
+                    a.ov[o] = b1 + a.c * (a.av[o] + dv);
+                    a.oh[o] = b2 + a.c * (a.ah[o] + dh);
+                    continue;
+                }
+                a.ou[o] = b0 + a.c * du;
+                a.ov[o] = b1 + a.c * dv;
+                a.oh[o] = b2 + a.c * dh;
+                if (a.acc_mode == 1) {
+                    a.au[o] = a.w * du;
+                    a.av[o] = a.w * dv;
+                    a.ah[o] = a.w * dh;
+                } else if (a.acc_mode == 2) {
+                    a.au[o] = a.au[o] + a.w * du;
+                    a.av[o] = a.av[o] + a.w * dv;
+                    a.ah[o] = a.ah[o] + a.w * dh;
+                }
+            }
         }
-        a.ou[o] = b0 + a.c * du;
-        a.ov[o] = b1 + a.c * dv;
-        a.oh[o] = b2 + a.c * dh;
-        if (a.acc_mode == 1) {
-            a.au[o] = a.w * du;
-            a.av[o] = a.w * dv;
-            a.ah[o] = a.w * dh;
-        } else if (a.acc_mode == 2) {
-            a.au[o] = a.au[o] + a.w * du;
-            a.av[o] = a.av[o] + a.w * dv;
-            a.ah[o] = a.ah[o] + a.w * dh;
-        }
+        __syncthreads();  // the next chunk overwrites Ms
     }
 }
 
@@ -144,7 +175,6 @@ struct ws_lpe {
     int64_t launches = 0;
     size_t es() const { return dtype == WS_F64 ? 8 : 4; }
     size_t cells() const { return (size_t)L * H * W; }
-    size_t lds_bytes() const { return (size_t)L * ws::kCX * ws::kCY * es(); }
 };
 
 namespace ws {
@@ -192,7 +222,7 @@ void stage(ws_lpe* m, void* const* in, void* const* out, T c, T w, int acc_mode)
     a.gp = (T)m->gp;
     a.f = (T)m->f;
     const dim3 grid((m->W + kTX - 1) / kTX, (m->H + kTY - 1) / kTY), block(kTX, kTY);
-    hipLaunchKernelGGL((lpe_stage_kernel<T>), grid, block, m->lds_bytes(), m->stream, a);
+    hipLaunchKernelGGL((lpe_stage_kernel<T>), grid, block, 0, m->stream, a);
     hck(hipGetLastError(), "lpe_stage_kernel");
     m->launches += 1;
 }
@@ -241,8 +271,6 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
         if (cfg->grid_width < 3 || cfg->grid_height < 3 || cfg->num_levels < 1)
             throw AbiError(WS_ERR_INVALID, "layered model needs a grid of at least 3 x 3 and one layer");
         if (!(cfg->dx > 0 && cfg->dy > 0)) throw AbiError(WS_ERR_INVALID, "Grid spacing must be positive");
-        const size_t lds = (size_t)cfg->num_levels * ws::kCX * ws::kCY * (cfg->double_precision ? 8 : 4);
-        if (lds > 160 * 1024) throw AbiError(WS_ERR_INVALID, "too many layers for the LDS column tile");
         ws::abi_set_device(cfg->device_id);
         ws_lpe* m = new ws_lpe;
         m->W = cfg->grid_width;
@@ -269,12 +297,6 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
                 }
             for (void** grp : {m->A, m->B, m->acc})
                 for (int i = 0; i < 3; ++i) ws::hck(hipMalloc(&grp[i], fb), "hipMalloc");
-            if (m->lds_bytes() > 64 * 1024) {
-                const void* fn = m->dtype == WS_F64 ? (const void*)ws::lpe_stage_kernel<double>
-                                                    : (const void*)ws::lpe_stage_kernel<float>;
-                ws::hck(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)m->lds_bytes()),
-                        "hipFuncSetAttribute");
-            }
         } catch (...) {
             ws::lpe_free(m);
             throw;

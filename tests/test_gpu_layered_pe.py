@@ -39,7 +39,7 @@ def rel(a, b):
     return float(np.linalg.norm(a.astype(np.float64) - b) / max(np.linalg.norm(b), 1e-300))
 
 
-@pytest.mark.parametrize("W,H,L", [(64, 48, 4), (37, 29, 3), (70, 20, 1), (40, 40, 32)])
+@pytest.mark.parametrize("W,H,L", [(64, 48, 4), (37, 29, 3), (70, 20, 1), (40, 40, 32), (33, 9, 11)])
 @pytest.mark.parametrize("method", [0, 1, 2])
 def test_matches_oracle_fp64(W, H, L, method):
     m = model(W, H, L, method, True, dx=1000.0, dy=1300.0)
@@ -114,7 +114,6 @@ def test_errors():
     with pytest.raises(RuntimeError):
         m.set_field("h", np.zeros((2, 16, 15)))
     c = ws.SimulationConfig()
-    c.grid_width, c.grid_height, c.num_levels = 16, 16, 200
-    c.double_precision = True
+    c.grid_width, c.grid_height, c.num_levels = 2, 16, 4
     with pytest.raises(ValueError):
         ws.LayeredPrimitiveEquationsModel(c)
