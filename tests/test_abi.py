@@ -90,7 +90,26 @@ def test_no_device_fails_loudly():
         ws.WeatherSimulation(ws.SimulationConfig())
     with pytest.raises(_native.WsDeviceError):
         ws.WeatherSimulationWrapper(16, 16)
+    with pytest.raises(_native.WsDeviceError):
+        ws.BarotropicVorticityModel(ws.SimulationConfig())
+    with pytest.raises(_native.WsDeviceError):
+        ws.LayeredPrimitiveEquationsModel(ws.SimulationConfig())
     assert ws.is_cuda_available() is False
+
+
+def test_physics_models_validate_before_touching_the_device():
+    c = ws.SimulationConfig()
+    c.grid_width = 2
+    with pytest.raises(ValueError):
+        ws.BarotropicVorticityModel(c)
+    with pytest.raises(ValueError):
+        ws.LayeredPrimitiveEquationsModel(c)
+    c = ws.SimulationConfig()
+    c.dx = 0.0
+    with pytest.raises(ValueError):
+        ws.BarotropicVorticityModel(c)
+    with pytest.raises(TypeError):
+        ws.BarotropicVorticityModel({"grid_width": 64})
 
 
 def test_slab_partition_is_balanced_and_covers_rows():
