@@ -59,6 +59,9 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
 #ifndef WS_DPPY_MINW
 #define WS_DPPY_MINW 1  // LDS-resident y: 133 VGPRs (RK4 fp64) fit 3 waves per SIMD unforced
 #endif
+#ifndef WS_SCHED_EVERY
+#define WS_SCHED_EVERY 1
+#endif
 #ifndef WS_DPPY_GROUPS
 #define WS_DPPY_GROUPS 1  // LDS-resident y: DMA groups in flight (ring 6 rows fp64 / 12 fp32 at 1)
 #endif
@@ -270,7 +273,9 @@ __global__ __launch_bounds__(kWave, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fu
         // keep the row's loads at the head of the body: the scheduler would otherwise sink
         // them below the stencil math, shortening the prefetch distance
 #if WS_SCHED_BARRIER
-        __builtin_amdgcn_sched_barrier(0);
+        // (every WS_SCHED_EVERY-th body: between barriers the scheduler may interleave
+        // consecutive rows' stage chains)
+        if constexpr (P % WS_SCHED_EVERY == 0) __builtin_amdgcn_sched_barrier(0);
 #endif
         if constexpr (WS_ABLATE == 2) {
             store_row(R - NST, YROW(-NST));
