@@ -253,9 +253,12 @@ def test_full_size_digests(name):
                         f"|ref|={ref_l2!r})")
 
 
-def test_pe_levels_match_reference_per_level():
+@pytest.mark.parametrize("aux", ["1", "0"])
+def test_pe_levels_match_reference_per_level(aux, monkeypatch):
     """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
-    must equal a standalone reference run of that level (bitwise)."""
+    must equal a standalone reference run of that level (bitwise) -- with the T / P update
+    on the second stream (WS_PE_AUX=1, the default) and on the main stream."""
+    monkeypatch.setenv("WS_PE_AUX", aux)
     digests = large_digests()
     L = 32
     sim = make_sim(1024, 1024, 2, 2, False, max_time=1e30, levels=L)
