@@ -59,6 +59,10 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
 #ifndef WS_DPPY_MINW
 #define WS_DPPY_MINW 1  // LDS-resident y: 133 VGPRs (RK4 fp64) fit 3 waves per SIMD unforced
 #endif
+#ifndef WS_DPP_WPB
+#define WS_DPP_WPB 1  // waves per workgroup: >1 puts adjacent strips on one CU (shared L1 for the overlap)
+#endif
+constexpr int kWpb = WS_DPP_WPB;
 #ifndef WS_SCHED_EVERY
 #define WS_SCHED_EVERY 1
 #endif
@@ -84,7 +88,7 @@ constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 
 // one group ahead) and the VGPR ring of y rows is gone, which is what lets the kernel fit
 // three waves per SIMD (<= 168 VGPRs) where the others fit two.
 template <typename T, int NST, int POW2, int PF>
-__global__ __launch_bounds__(kWave, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
+__global__ __launch_bounds__(kWave * kWpb, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fused_dpp_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
     constexpr bool kDma = PF <= 0;
     constexpr bool kLdsY = PF < 0;
@@ -108,13 +112,16 @@ __global__ __launch_bounds__(kWave, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fu
     // when read in place), and the DMAs issued in between (including the reading body's own)
     constexpr int kWaitN = kLdsY ? 3 * kD + 3 * (kD / kG) : 3 * (kD - 1) + 3 * ((kD - 1) / (kG > 0 ? kG : 1));
 
-    const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
+    // XCD-aware: neighbouring strips share an L2 (and with kWpb > 1 a CU)
+    const int w = xcd_work_item() * kWpb + (int)threadIdx.x / kWave;
+    if (w >= nstrips * nsegs * g.L) return;  // the last workgroup's spare waves (no barriers)
     const int strip = w % nstrips;
     int y0, y1;
     fused_rows(a, (w / nstrips) % nsegs, y0, y1);
     const int level = w / (nstrips * nsegs);
 
-    const int lane = threadIdx.x;
+    const int lane = (int)threadIdx.x % kWave;
+    const int wave_id = (int)threadIdx.x / kWave;  // wave within the workgroup (its LDS ring)
     // left margin: the cone (NST), for DMA rounded up to whole 16-byte chunks
     constexpr int kM = kDma ? (NST + kG - 1) / kG * kG : NST;
     const int out_w = a.out_w;
@@ -173,7 +180,8 @@ __global__ __launch_bounds__(kWave, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) void fu
 
     // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG
     // consecutive slots (64 lanes x 16 B = kG rows of 64 columns)
-    __shared__ __attribute__((aligned(16))) T ring[kDma ? 3 : 1][kDma ? kNR : 1][kWave];
+    __shared__ __attribute__((aligned(16))) T rings[kWpb][kDma ? 3 : 1][kDma ? kNR : 1][kWave];
+    auto& ring = rings[wave_id];
     const int dk = lane / (kWave / kG);                          // row of the group this lane fetches
     const int dcol = (strip * out_w - kM) * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // byte column (16-B aligned)
     auto dma = [&](int q, int slot) {  // rows q .. q + kG - 1 into slots slot .. slot + kG - 1
@@ -379,7 +387,7 @@ hipError_t launch_dpp_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hi
     // dropped-store voffset is 2^31
     const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 3 * kUMax) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)nblocks), block(kWave);
+    const dim3 grid((unsigned)((nblocks + kWpb - 1) / kWpb)), block(kWave * kWpb);
     const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
 #define WS_DPP_GO(N, P2) hipLaunchKernelGGL((fused_dpp_kernel<T, N, P2, PF>), grid, block, 0, s, a, g, nstrips, nsegs)
 #define WS_DPP_LAUNCH(N)                                  \
