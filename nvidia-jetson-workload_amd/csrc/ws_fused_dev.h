@@ -36,8 +36,14 @@ __device__ __forceinline__ V buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
 }
 template <typename V>
 __device__ __forceinline__ void buf_store_nt(V v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    // 16-byte stores take the row offset in voffset, soffset = 0: a dwordx4 store's data
+    // VGPRs rewritten by the next VALU instruction need one wait state, and the compiler only
+    // inserts it when soffset is not a register -- with an SGPR soffset it scheduled
+    // `v_add v0, ...` straight after `buffer_store_dwordx4 v[0:3], ..., s10` and corrupted
+    // the pair's first element (found on gfx950 at large grids). kDropped + soff stays past
+    // every range (soff < 2^31), so dropped stores stay dropped.
     if constexpr (sizeof(V) == 16)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)voff, (int)soff, kNT);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)(voff + soff), 0, kNT);
     else if constexpr (sizeof(V) == 8)
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
     else

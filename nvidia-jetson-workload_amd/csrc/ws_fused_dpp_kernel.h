@@ -107,10 +107,13 @@ __global__ __launch_bounds__(kWave * kWpb, PF < 0 ? WS_DPPY_MINW : WS_DPP_MINW) 
     static_assert(!kDma || (kU % kG == 0 && kU % 2 == 0 && kNR >= kD + kG + (kLdsY ? 2 : 0) && kD % kG == 0 &&
                             (kLdsY || kU > kG + 4)),
                   "DMA ring");
-    // younger vector-memory ops than a group's DMAs when that group is read: the stores of
-    // the bodies from its issue on (kD - 1 of them when read one body early into VGPRs, kD
-    // when read in place), and the DMAs issued in between (including the reading body's own)
-    constexpr int kWaitN = kLdsY ? 3 * kD + 3 * (kD / kG) : 3 * (kD - 1) + 3 * ((kD - 1) / (kG > 0 ? kG : 1));
+    // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory ops
+    // issued after them that are LOADS (the DMAs issued in between, including the reading
+    // body's own). Stores are not counted: a store may complete before an older load, so an
+    // outstanding count that includes them can drop below the threshold while the group is
+    // still in flight (seen as stale rows at 4096^2). Loads complete in order, so at most
+    // kWaitN outstanding ops means every older load -- the group -- has landed.
+    constexpr int kWaitN = kLdsY ? 3 * (kD / kG) : 3 * ((kD - 1) / (kG > 0 ? kG : 1));
 
     // XCD-aware: neighbouring strips share an L2 (and with kWpb > 1 a CU)
     const int w = xcd_work_item() * kWpb + (int)threadIdx.x / kWave;

@@ -83,9 +83,11 @@ __global__ __launch_bounds__(kWave, WS_X2Y_MINW) void fused_x2y_kernel(FusedArgs
     constexpr int kNR = 6;                         // LDS ring rows: R-2 .. R+kD+kG-1 fit
     constexpr int kU = kNR;                        // march unroll: ring slot == phase
     static_assert(kNR >= kD + kG + 2 && kU % kG == 0 && kU % 2 == 0 && kD % kG == 0, "ring");
-    // younger vector-memory ops than a group's DMAs when it is read in place: the 3 stores of
-    // each of the kD bodies since, the DMAs issued in between (incl. the reading body's)
-    constexpr int kWaitN = 3 * kD + 3 * (kD / kG);
+    // wait until at most the younger DMA loads are outstanding (the DMAs issued since the
+    // group, incl. the reading body's): loads complete in order, stores do not (a younger
+    // store can retire before an older load), so stores are not counted -- see
+    // ws_fused_dpp_kernel.h
+    constexpr int kWaitN = 3 * (kD / kG);
     constexpr int kM = margin<T>(NST);
     const int out_w = a.out_w;
 
