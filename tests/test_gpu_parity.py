@@ -304,6 +304,40 @@ def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, monkeypatch):
         np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
 
 
+_LARGE_REF = {}
+
+
+@pytest.mark.parametrize("kernel", ["x2", "dpp", "dppdma", "dppy", "x2y", "lds"])
+@pytest.mark.parametrize("case", ["rk4_f64", "rk2_f32"])
+def test_every_variant_large_grid_vs_oracle(case, kernel, monkeypatch):
+    """Every variant pinned at a grid large enough that late-dispatched workgroups run
+    beside finished ones (4096 x 2048, segments of 64 rows): a 16-byte store data hazard
+    corrupted fused_x2y here and never at the small tiling sizes; bitwise vs the oracle."""
+    from oracle.ws_oracle import OracleSim
+
+    method, fp64 = (2, True) if case == "rk4_f64" else (1, False)
+    monkeypatch.setenv("WS_SEG_ROWS", "64")
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    W, H, steps = 4096, 2048, 2
+    sim = make_sim(W, H, 0, method, fp64, dx=1.0, dy=1.0, f=1e-4, max_time=1e30)
+    sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
+    sim.initialize()
+    if case not in _LARGE_REF:
+        g = sim.get_current_grid()
+        ref = OracleSim(W, H, 0, method, coriolis_f=1e-4, max_time=1e30, precision="f64" if fp64 else "f32")
+        ref.initialize()
+        u, v = g.get_velocity_field()
+        for k, a in (("u", u), ("v", v), ("h", g.get_height_field())):
+            ref.set_field(k, a)
+        ref.run(steps)
+        _LARGE_REF[case] = {k: ref.get_field(k) for k in ("u", "v", "h")}
+    sim.run(steps)
+    got = state(sim.get_current_grid())
+    for k in ("u", "v", "h"):
+        bad = np.argwhere(got[k] != _LARGE_REF[case][k])
+        assert len(bad) == 0, f"{kernel} {case} {k}: {len(bad)} cells differ, first {bad[:4].tolist()}"
+
+
 def test_fused_non_pow2_spacing_vs_oracle():
     """dx = 0.75: 2dx is not a power of two -> the IEEE-divide instantiation."""
     from oracle.ws_oracle import OracleSim
