@@ -154,9 +154,10 @@ def cpu_baseline(conf, method, budget_s=20.0):
 
 def bvort_words_per_cell(method, W, H):
     """Algorithmic traffic of one barotropic step in words per cell: per RK stage an R2C
-    (read W*H reals, write (W/2+1)*H complex), the spectral scale (read + write the
-    spectrum), a C2R (read the spectrum, write W*H reals) and the stage stencil (read zeta_s,
-    psi, zeta_0 [+ acc], write zeta_out [+ acc])."""
+    (read W*H reals, write (W/2+1)*H complex), the column pass (read + write the spectrum;
+    the hipFFT path's separate spectral scale moves the same bytes), a C2R (read the
+    spectrum, write W*H reals) and the stage stencil (read zeta_s, psi, zeta_0 [+ acc],
+    write zeta_out [+ acc])."""
     spec = 2.0 * (W // 2 + 1) * H / (W * H)  # complex spectrum, in real words per cell
     fft = (1 + spec) + 2 * spec + (spec + 1)
     stencil = {0: [4], 1: [4, 4], 2: [5, 6, 6, 5]}[method]
@@ -207,7 +208,7 @@ def bench_bvort(args, conf, method, world):
                    "integrator": args.method, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "whole step (hipFFT R2C/C2R + spectral scale + bv_stage_kernel)",
+                     "kernel": "whole step (LDS-FFT Poisson: bv_rowfft_fwd + bv_colsolve + bv_rowfft_inv, then bv_stage_kernel)",
                      "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
                      "note": "device time of the run (hipEvents on the model's stream) per step; "
                              "bytes = bvort_words_per_cell x cells"},

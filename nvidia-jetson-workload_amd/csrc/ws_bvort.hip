@@ -16,6 +16,7 @@
 #include <hipfft/hipfft.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -126,6 +127,198 @@ __global__ __launch_bounds__(256) void bv_velocity_kernel(const T* psi, T* u, T*
     v[o] = (pe - pw) * inv2dx;
 }
 
+// ---- Poisson solve by LDS-resident FFTs (power-of-two W, H <= 4096) --------------------
+// Three passes, each reading and writing the field once (hipFFT's 2-D plan is eight kernels
+// per R2C / C2R pair, two of them transposes):
+//   1. bv_rowfft_fwd: two real rows a, b as one complex FFT z = a + i b (radix-2 DIT in
+//      LDS), split into the half spectra A(k), B(k), k = 0..W/2 -> spec[l][k];
+//   2. bv_colsolve:  CW adjacent spectrum columns: forward FFT along y (DIT), scale by
+//      norm / lambda(k, l) (the (0, 0) mode -> 0), inverse FFT along y (DIF, bit-reversed
+//      result written back in natural order);
+//   3. bv_rowfft_inv: Z = A + i B over the full Hermitian extension, inverse FFT (DIF),
+//      real part -> row a of psi, imaginary part -> row b.
+// Twiddles tw[j] = exp(-2 pi i j / N), j < N/2, computed on the host in double.
+template <typename T>
+struct Cx {
+    T x, y;
+};
+
+// LDS index padding: one spare element per 16 breaks the power-of-two strides of the
+// bit-reversed scatter and the short-span passes out of a single bank group
+__device__ __forceinline__ int P(int i) { return i + (i >> 4); }
+__host__ __device__ constexpr size_t padded(size_t n) { return n + n / 16 + 1; }
+
+__device__ __forceinline__ int bitrev(int i, int logn) { return (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - logn)); }
+
+// Radix-2 stages taken R at a time in registers (one LDS pass and one barrier per R stages):
+// a thread owns the 2^R elements base + j + m h (m < 2^R, j < h) that those stages combine.
+// DIT: stages s .. s+R-1 (h = 2^(s-1)); input bit-reversed, output natural after all passes.
+template <typename T, bool INV, int R>
+__device__ __forceinline__ void dit_pass(Cx<T>* a, const Cx<T>* tw, int n, int logn, int s, int ncol) {
+    constexpr int M = 1 << R;
+    const int h = 1 << (s - 1);
+    const int lg = logn - R;  // log2(groups per column)
+    for (int g = threadIdx.x; g < (ncol << lg); g += blockDim.x) {
+        const int c = g >> lg, gg = g & ((1 << lg) - 1);
+        const int j = gg & (h - 1);
+        const int base = c * n + ((gg >> (s - 1)) << (s - 1 + R)) + j;
+        Cx<T> x[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) x[m] = a[P(base + m * h)];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            const int hs = 1 << t;
+            const int tstep = n >> (s + t);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                if (m & hs) continue;
+                Cx<T> w = tw[(j + (m & (hs - 1)) * h) * tstep];
+                if (INV) w.y = -w.y;
+                const Cx<T> v = x[m + hs];
+                const Cx<T> p{v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x};
+                x[m + hs] = Cx<T>{x[m].x - p.x, x[m].y - p.y};
+                x[m] = Cx<T>{x[m].x + p.x, x[m].y + p.y};
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) a[P(base + m * h)] = x[m];
+    }
+    __syncthreads();
+}
+
+// DIF: stages s, s-1, .., s-R+1 (h = 2^(s-R), the smallest half); input natural, output
+// bit-reversed after all passes.
+template <typename T, bool INV, int R>
+__device__ __forceinline__ void dif_pass(Cx<T>* a, const Cx<T>* tw, int n, int logn, int s, int ncol) {
+    constexpr int M = 1 << R;
+    const int lh = s - R;
+    const int h = 1 << lh;
+    const int lg = logn - R;
+    for (int g = threadIdx.x; g < (ncol << lg); g += blockDim.x) {
+        const int c = g >> lg, gg = g & ((1 << lg) - 1);
+        const int j = gg & (h - 1);
+        const int base = c * n + ((gg >> lh) << (lh + R)) + j;
+        Cx<T> x[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) x[m] = a[P(base + m * h)];
+#pragma unroll
+        for (int t = R - 1; t >= 0; --t) {
+            const int hs = 1 << t;
+            const int tstep = n >> (lh + 1 + t);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                if (m & hs) continue;
+                Cx<T> w = tw[(j + (m & (hs - 1)) * h) * tstep];
+                if (INV) w.y = -w.y;
+                const Cx<T> u = x[m], v = x[m + hs];
+                const Cx<T> d{u.x - v.x, u.y - v.y};
+                x[m] = Cx<T>{u.x + v.x, u.y + v.y};
+                x[m + hs] = Cx<T>{d.x * w.x - d.y * w.y, d.x * w.y + d.y * w.x};
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) a[P(base + m * h)] = x[m];
+    }
+    __syncthreads();
+}
+
+// radix-2 decimation in time over ncol columns of length n (column c at a + c * n), input in
+// bit-reversed order, output natural; forward (INV = false) or unscaled inverse
+template <typename T, bool INV>
+__device__ void fft_dit(Cx<T>* a, const Cx<T>* tw, int n, int logn, int ncol) {
+    int s = 1;
+    for (; logn - s + 1 >= 3; s += 3) dit_pass<T, INV, 3>(a, tw, n, logn, s, ncol);
+    if (logn - s + 1 == 2) dit_pass<T, INV, 2>(a, tw, n, logn, s, ncol);
+    else if (logn - s + 1 == 1) dit_pass<T, INV, 1>(a, tw, n, logn, s, ncol);
+}
+
+// radix-2 decimation in frequency: input natural, output bit-reversed
+template <typename T, bool INV>
+__device__ void fft_dif(Cx<T>* a, const Cx<T>* tw, int n, int logn, int ncol) {
+    int s = logn;
+    for (; s >= 3; s -= 3) dif_pass<T, INV, 3>(a, tw, n, logn, s, ncol);
+    if (s == 2) dif_pass<T, INV, 2>(a, tw, n, logn, s, ncol);
+    else if (s == 1) dif_pass<T, INV, 1>(a, tw, n, logn, s, ncol);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bv_rowfft_fwd(const T* z, Cx<T>* spec, const Cx<T>* tw, int W, int logw) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    Cx<T>* a = (Cx<T>*)smem;
+    Cx<T>* twl = a + padded(W);  // twiddles staged in LDS: every pass reads them
+    const int nk = W / 2 + 1;
+    const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
+    for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
+    for (int i = threadIdx.x; i < W; i += blockDim.x) a[P(bitrev(i, logw))] = Cx<T>{z[r0 * W + i], z[r1 * W + i]};
+    __syncthreads();
+    fft_dit<T, false>(a, twl, W, logw, 1);
+    const T h = T(0.5);
+    for (int k = threadIdx.x; k < nk; k += blockDim.x) {
+        const Cx<T> zk = a[P(k)], zm = a[P((W - k) & (W - 1))];  // Z(k), Z(W - k)
+        // A = (Z(k) + conj Z(W-k)) / 2, B = (Z(k) - conj Z(W-k)) / 2i
+        spec[r0 * nk + k] = Cx<T>{(zk.x + zm.x) * h, (zk.y - zm.y) * h};
+        spec[r1 * nk + k] = Cx<T>{(zk.y + zm.y) * h, (zm.x - zk.x) * h};
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw, const T* ax, const T* ay, int nk,
+                                                    int H, int logh, int cw, T norm) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    Cx<T>* a = (Cx<T>*)smem;
+    Cx<T>* twl = a + padded((size_t)cw * H);
+    const int k0 = blockIdx.x * cw;
+    const int ncol = min(cw, nk - k0);
+    for (int i = threadIdx.x; i < H / 2; i += blockDim.x) twl[i] = tw[i];
+    for (int i = threadIdx.x; i < H * cw; i += blockDim.x) {
+        const int l = i / cw, c = i - l * cw;
+        if (c < ncol) a[P(c * H + bitrev(l, logh))] = spec[(int64_t)l * nk + k0 + c];
+    }
+    __syncthreads();
+    fft_dit<T, false>(a, twl, H, logh, ncol);
+    for (int i = threadIdx.x; i < H * ncol; i += blockDim.x) {
+        const int c = i / H, l = i - c * H;
+        const int k = k0 + c;
+        const T m = (k == 0 && l == 0) ? T(0) : norm / (ax[k] + ay[l]);
+        a[P(i)].x *= m;
+        a[P(i)].y *= m;
+    }
+    __syncthreads();
+    fft_dif<T, true>(a, twl, H, logh, ncol);
+    for (int i = threadIdx.x; i < H * cw; i += blockDim.x) {
+        const int l = i / cw, c = i - l * cw;
+        if (c < ncol) spec[(int64_t)l * nk + k0 + c] = a[P(c * H + bitrev(l, logh))];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bv_rowfft_inv(const Cx<T>* spec, T* psi, const Cx<T>* tw, int W, int logw) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    Cx<T>* a = (Cx<T>*)smem;
+    Cx<T>* twl = a + padded(W);
+    const int nk = W / 2 + 1;
+    const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
+    for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
+    for (int k = threadIdx.x; k < W; k += blockDim.x) {
+        const bool lo = k < nk;
+        const int kk = lo ? k : W - k;
+        Cx<T> A = spec[r0 * nk + kk], B = spec[r1 * nk + kk];
+        if (kk == 0 || kk == W / 2) A.y = B.y = T(0);  // C2R: the real bins' imaginary parts are ignored
+        if (!lo) {
+            A.y = -A.y;
+            B.y = -B.y;
+        }
+        a[P(k)] = Cx<T>{A.x - B.y, A.y + B.x};  // Z = A + i B
+    }
+    __syncthreads();
+    fft_dif<T, true>(a, twl, W, logw, 1);
+    for (int i = threadIdx.x; i < W; i += blockDim.x) {
+        const Cx<T> v = a[P(bitrev(i, logw))];
+        psi[r0 * W + i] = v.x;
+        psi[r1 * W + i] = v.y;
+    }
+}
+
 void hck(hipError_t e, const char* what) {
     if (e != hipSuccess) throw AbiError(WS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -147,6 +340,10 @@ struct ws_bvort {
     void* z[2] = {nullptr, nullptr};
     void *A = nullptr, *B = nullptr, *psi = nullptr, *acc = nullptr, *spec = nullptr, *ax = nullptr, *ay = nullptr;
     void *u = nullptr, *v = nullptr;
+    // LDS-FFT Poisson path (power-of-two W, H; WS_BV_FFT=hipfft selects the library)
+    bool lds_fft = false;
+    void *twW = nullptr, *twH = nullptr;
+    int logw = 0, logh = 0, cw = 1;
     int cur = 0;
     bool psi_current = false;  // psi holds the streamfunction of z[cur]
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -161,7 +358,7 @@ namespace ws {
 namespace {
 
 void bv_free(ws_bvort* b) {
-    for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay, b->u, b->v})
+    for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay, b->u, b->v, b->twW, b->twH})
         if (p) (void)hipFree(p);
     if (b->have_r2c) hipfftDestroy(b->r2c);
     if (b->have_c2r) hipfftDestroy(b->c2r);
@@ -180,11 +377,43 @@ void upload_eigen(ws_bvort* b) {
     for (int l = 0; l < b->H; ++l) ay[l] = (T)((2.0 * std::cos(2.0 * pi * l / b->H) - 2.0) / (b->dy * b->dy));
     hck(hipMemcpy(b->ax, ax.data(), nk * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
     hck(hipMemcpy(b->ay, ay.data(), b->H * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+    if (b->lds_fft) {
+        auto twiddles = [&](int n, void* dst) {
+            std::vector<T> t((size_t)n);  // n / 2 complex
+            for (int j = 0; j < n / 2; ++j) {
+                t[2 * j] = (T)std::cos(2.0 * pi * j / n);
+                t[2 * j + 1] = (T)-std::sin(2.0 * pi * j / n);
+            }
+            hck(hipMemcpy(dst, t.data(), t.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy");
+        };
+        twiddles(b->W, b->twW);
+        twiddles(b->H, b->twH);
+    }
+}
+
+template <typename T>
+void poisson_lds(ws_bvort* b, const void* zin) {
+    const size_t cs = 2 * sizeof(T);
+    const int nk = b->W / 2 + 1;
+    Cx<T>* spec = (Cx<T>*)b->spec;
+    const size_t row_lds = (padded(b->W) + b->W / 2) * cs, col_lds = (padded((size_t)b->cw * b->H) + b->H / 2) * cs;
+    hipLaunchKernelGGL((bv_rowfft_fwd<T>), dim3(b->H / 2), dim3(256), row_lds, b->stream, (const T*)zin, spec,
+                       (const Cx<T>*)b->twW, b->W, b->logw);
+    hck(hipGetLastError(), "bv_rowfft_fwd");
+    hipLaunchKernelGGL((bv_colsolve<T>), dim3((nk + b->cw - 1) / b->cw), dim3(1024), col_lds,
+                       b->stream, spec, (const Cx<T>*)b->twH, (const T*)b->ax, (const T*)b->ay, nk, b->H, b->logh,
+                       b->cw, (T)(1.0 / ((double)b->W * b->H)));
+    hck(hipGetLastError(), "bv_colsolve");
+    hipLaunchKernelGGL((bv_rowfft_inv<T>), dim3(b->H / 2), dim3(256), row_lds, b->stream, (const Cx<T>*)spec,
+                       (T*)b->psi, (const Cx<T>*)b->twW, b->W, b->logw);
+    hck(hipGetLastError(), "bv_rowfft_inv");
+    b->launches += 3;
 }
 
 // psi = lap^-1 zin (spectral), on the model's stream
 template <typename T>
 void poisson(ws_bvort* b, const void* zin) {
+    if (b->lds_fft) return poisson_lds<T>(b, zin);
     const int nk = b->W / 2 + 1;
     if constexpr (sizeof(T) == 8) {
         fck(hipfftExecD2Z(b->r2c, (hipfftDoubleReal*)const_cast<void*>(zin), (hipfftDoubleComplex*)b->spec), "D2Z");
@@ -306,12 +535,37 @@ int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
             for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc})
                 ws::hck(hipMemset(p, 0, fb), "hipMemset");
             const bool f64 = b->dtype == WS_F64;
-            ws::fck(hipfftPlan2d(&b->r2c, b->H, b->W, f64 ? HIPFFT_D2Z : HIPFFT_R2C), "hipfftPlan2d");
-            b->have_r2c = true;
-            ws::fck(hipfftPlan2d(&b->c2r, b->H, b->W, f64 ? HIPFFT_Z2D : HIPFFT_C2R), "hipfftPlan2d");
-            b->have_c2r = true;
-            ws::fck(hipfftSetStream(b->r2c, b->stream), "hipfftSetStream");
-            ws::fck(hipfftSetStream(b->c2r, b->stream), "hipfftSetStream");
+            auto pow2 = [](int n) { return n >= 16 && n <= 4096 && (n & (n - 1)) == 0; };
+            const char* fe = std::getenv("WS_BV_FFT");
+            b->lds_fft = pow2(b->W) && pow2(b->H) && !(fe && std::strcmp(fe, "hipfft") == 0);
+            if (b->lds_fft) {
+                while ((1 << b->logw) < b->W) ++b->logw;
+                while ((1 << b->logh) < b->H) ++b->logh;
+                // adjacent spectrum columns per column-pass workgroup: <= 64 KB of LDS
+                const char* cwe = std::getenv("WS_BV_CW");
+                const size_t col_budget = cwe ? (size_t)std::atoi(cwe) * b->H * 2 * b->es() : 65536;
+                while (b->cw < 16 && (size_t)2 * b->cw * b->H * 2 * b->es() <= col_budget) b->cw *= 2;
+                // data + twiddles can pass the 64 KB default of dynamic LDS (fp64 rows of 4096)
+                const int lds_max = 160 * 1024;
+                if (f64) {
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_rowfft_fwd<double>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_rowfft_inv<double>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_colsolve<double>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                } else {
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_rowfft_fwd<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_rowfft_inv<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                    ws::hck(hipFuncSetAttribute((const void*)ws::bv_colsolve<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max), "hipFuncSetAttribute");
+                }
+                ws::hck(hipMalloc(&b->twW, (size_t)b->W * b->es()), "hipMalloc");
+                ws::hck(hipMalloc(&b->twH, (size_t)b->H * b->es()), "hipMalloc");
+            } else {
+                ws::fck(hipfftPlan2d(&b->r2c, b->H, b->W, f64 ? HIPFFT_D2Z : HIPFFT_R2C), "hipfftPlan2d");
+                b->have_r2c = true;
+                ws::fck(hipfftPlan2d(&b->c2r, b->H, b->W, f64 ? HIPFFT_Z2D : HIPFFT_C2R), "hipfftPlan2d");
+                b->have_c2r = true;
+                ws::fck(hipfftSetStream(b->r2c, b->stream), "hipfftSetStream");
+                ws::fck(hipfftSetStream(b->c2r, b->stream), "hipfftSetStream");
+            }
             if (f64) ws::upload_eigen<double>(b);
             else ws::upload_eigen<float>(b);
         } catch (...) {

@@ -107,3 +107,38 @@ def test_errors():
     c.grid_width, c.grid_height = 2, 10
     with pytest.raises(ValueError):
         ws.BarotropicVorticityModel(c)
+
+
+@pytest.mark.parametrize("W,H", [(64, 32), (256, 128), (16, 512), (4096, 16), (32, 4096), (2048, 2048)])
+@pytest.mark.parametrize("fft", ["lds", "hipfft"])
+def test_poisson_paths_fp64(W, H, fft, monkeypatch):
+    """Power-of-two grids take the three-pass LDS FFT Poisson solve (ws_bvort.hip
+    bv_rowfft_fwd / bv_colsolve / bv_rowfft_inv); WS_BV_FFT=hipfft the library's 2-D plans.
+    Both against the oracle's pocketfft solve and three RK4 steps. On the strongly
+    anisotropic grids (aspect 256) the Jacobian's derivatives along the long axis amplify
+    the FFTs' round-off (either FFT; ~3e-9 relative after three steps), hence 1e-8 there."""
+    if fft == "hipfft":
+        monkeypatch.setenv("WS_BV_FFT", "hipfft")
+    # the smooth field's streamfunction (and so its velocity) grows with the grid: keep the
+    # advective CFL number below ~0.5
+    kw = dict(dx=1.0, dy=1.25, dt=0.05 * min(1.0, 64.0 / max(W, H)), beta=0.3, nu=0.02)
+    m = model(W, H, 2, True, **kw)
+    z0 = smooth_field(W, H, seed=W + 3 * H)
+    z0 -= z0.mean()
+    m.set_vorticity(z0)
+    assert rel(m.get_streamfunction(), bo.poisson(z0, kw["dx"], kw["dy"])) < 1e-12
+    m.run(3)
+    want = bo.run(z0, 3, kw["dt"], kw["dx"], kw["dy"], kw["beta"], kw["nu"], 2)
+    assert rel(m.get_vorticity_field(), want) < (1e-11 if max(W, H) <= 8 * min(W, H) else 1e-8)
+
+
+@pytest.mark.parametrize("W,H", [(256, 128), (2048, 2048)])
+def test_poisson_lds_fft_fp32(W, H):
+    dt = 0.05 * min(1.0, 64.0 / max(W, H))
+    m = model(W, H, 2, False, dt=dt, beta=0.2, nu=0.01)
+    z0 = smooth_field(W, H, seed=7)
+    z0 -= z0.mean()
+    m.set_vorticity(z0)
+    assert rel(m.get_streamfunction(), bo.poisson(z0, 1.0, 1.0)) < 1e-5
+    m.run(5)
+    assert rel(m.get_vorticity_field(), bo.run(z0, 5, dt, 1.0, 1.0, 0.2, 0.01, 2)) < 1e-4
