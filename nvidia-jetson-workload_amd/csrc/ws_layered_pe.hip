@@ -24,7 +24,13 @@
 namespace ws {
 namespace {
 
-constexpr int kTX = 32, kTY = 8;
+#ifndef WS_LPE_TX
+#define WS_LPE_TX 128  // c4p RK4 fp32 tile sweep 32x8 / 64x8 / 64x16 / 128x4 / 128x8 -> 15.5 / 18.1 / 18.2 / 18.4 / 18.6 Gcell/s
+#endif
+#ifndef WS_LPE_TY
+#define WS_LPE_TY 8
+#endif
+constexpr int kTX = WS_LPE_TX, kTY = WS_LPE_TY;  // output tile (workgroup = kTX x kTY threads)
 constexpr int kCX = kTX + 2, kCY = kTY + 2;  // tile + halo columns
 
 template <typename T>
@@ -98,12 +104,18 @@ __global__ __launch_bounds__(kTX* kTY) void lpe_stage_kernel(LpeArgs<T> a) {
             const int c = tid + i * kTX * kTY;
             if (c >= kCX * kCY) continue;
             const int lxc = c % kCX, lyc = c / kCX;
-            for (int j = 0; j < nk; ++j) {
+            // the chunk's thicknesses first (independent loads in flight together), then the scan
+            T hv[kChunk];
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) hv[j] = j < nk ? hc[i][(int64_t)(k0 + j) * a.lstride] : T(0);
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) {
+                if (j >= nk) break;
                 const int k = k0 + j;
                 const T eta = total[i] - prefix[i];
                 Mprev[i] = k == 0 ? a.g * eta : Mprev[i] + a.gp * eta;
                 Ms[j][lyc][lxc] = Mprev[i];
-                prefix[i] = prefix[i] + hc[i][(int64_t)k * a.lstride];
+                prefix[i] = prefix[i] + hv[j];
             }
         }
         __syncthreads();
