@@ -58,7 +58,7 @@ __device__ __forceinline__ int wrapi(int i, int n) { return i < 0 ? i + n : (i >
 #endif
 constexpr int kChunk = WS_LPE_CHUNK;
 #ifndef WS_LPE_UNROLL
-#define WS_LPE_UNROLL 2  // measured at 1024^2 x 32 fp32 RK4: 1 / 2 / 4 / 8 -> 15.2 / 16.2 / 14.2 / 15.5 Gcell/s
+#define WS_LPE_UNROLL 1  // 1024^2 x 32 fp32 RK4: 32x8 tile 1 / 2 / 4 / 8 -> 15.2 / 16.2 / 14.2 / 15.5; 128x8 tile 1 / 2 -> 18.8 / 17.6 Gcell/s
 #endif
 constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
 
