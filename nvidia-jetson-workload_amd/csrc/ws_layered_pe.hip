@@ -28,7 +28,7 @@ namespace {
 #define WS_LPE_TX 128  // c4p RK4 fp32 tile sweep 32x8 / 64x8 / 64x16 / 128x4 / 128x8 -> 15.5 / 18.1 / 18.2 / 18.4 / 18.6 Gcell/s
 #endif
 #ifndef WS_LPE_TY
-#define WS_LPE_TY 8
+#define WS_LPE_TY 4  // 128x4 (2 waves per SIMD) so the 80-VGPR fp32 kernel runs 3 workgroups per CU
 #endif
 constexpr int kTX = WS_LPE_TX, kTY = WS_LPE_TY;  // output tile (workgroup = kTX x kTY threads)
 constexpr int kCX = kTX + 2, kCY = kTY + 2;  // tile + halo columns
@@ -62,8 +62,13 @@ constexpr int kChunk = WS_LPE_CHUNK;
 #endif
 constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
 
+#ifndef WS_LPE_WAVES
+#define WS_LPE_WAVES 6  // fp32: VGPRs capped at 80 -> 6 waves/SIMD (128x4 tile: 18.5 -> 19.1-19.3 Gcell/s; 8 waves spills: 14.5); fp64 unconstrained
+#endif
+
 template <typename T>
-__global__ __launch_bounds__(kTX* kTY) void lpe_stage_kernel(LpeArgs<T> a) {
+__global__ __launch_bounds__(kTX* kTY) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? WS_LPE_WAVES : 1)))
+void lpe_stage_kernel(LpeArgs<T> a) {
     __shared__ T Ms[kChunk][kCY][kCX];
     const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
     const int tid = threadIdx.y * kTX + threadIdx.x;
