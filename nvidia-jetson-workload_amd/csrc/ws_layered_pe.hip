@@ -62,6 +62,9 @@ constexpr int kChunk = WS_LPE_CHUNK;
 #endif
 constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
 
+#ifndef WS_LPE_HLDS
+#define WS_LPE_HLDS 1  // the walk takes h's neighbours from an LDS copy of the scan's loads (0: from L1/L2; c4p 20.5 -> 21.2 Gcell/s)
+#endif
 #ifndef WS_LPE_WAVES
 #define WS_LPE_WAVES 6  // fp32: VGPRs capped at 80 -> 6 waves/SIMD (128x4 tile: 18.5 -> 19.1-19.3 Gcell/s; 8 waves spills: 14.5); fp64 unconstrained
 #endif
@@ -70,6 +73,9 @@ template <typename T>
 __global__ __launch_bounds__(kTX* kTY) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? WS_LPE_WAVES : 1)))
 void lpe_stage_kernel(LpeArgs<T> a) {
     __shared__ T Ms[kChunk][kCY][kCX];
+#if WS_LPE_HLDS
+    __shared__ T Hs[kChunk][kCY][kCX];  // the chunk's h tile + halo, loaded once by the scan
+#endif
     const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
     const int tid = threadIdx.y * kTX + threadIdx.x;
     // scan state of this thread's columns of the tile + halo (oracle order: total = h_0 +
@@ -120,6 +126,9 @@ void lpe_stage_kernel(LpeArgs<T> a) {
                 const T eta = total[i] - prefix[i];
                 Mprev[i] = k == 0 ? a.g * eta : Mprev[i] + a.gp * eta;
                 Ms[j][lyc][lxc] = Mprev[i];
+#if WS_LPE_HLDS
+                Hs[j][lyc][lxc] = hv[j];
+#endif
                 prefix[i] = prefix[i] + hv[j];
             }
         }
@@ -134,7 +143,13 @@ void lpe_stage_kernel(LpeArgs<T> a) {
                 const T u = U[oc], v = V[oc];
                 const T ue = U[oe], uw = U[ow], un = U[on], us = U[os];
                 const T ve = V[oe], vw = V[ow], vn = V[on], vs = V[os];
+#if WS_LPE_HLDS
+                (void)Hh;
+                const T he = Hs[j][ly][lx + 1], hw = Hs[j][ly][lx - 1];
+                const T hn = Hs[j][ly + 1][lx], hs = Hs[j][ly - 1][lx];
+#else
                 const T he = Hh[oe], hw = Hh[ow], hn = Hh[on], hs = Hh[os];
+#endif
                 const T Me = Ms[j][ly][lx + 1], Mw = Ms[j][ly][lx - 1];
                 const T Mn = Ms[j][ly + 1][lx], Mso = Ms[j][ly - 1][lx];
                 const T u_x = (ue - uw) * a.ix, u_y = (un - us) * a.iy;
