@@ -226,6 +226,28 @@ int ws_group_destroy(ws_group_t* group);
 int ws_group_slab(ws_group_t* group, int32_t rank, ws_sim_t** sim, int32_t* row0, int32_t* rows);
 int ws_group_run(ws_group_t* group, int32_t num_steps, int32_t* steps_taken);
 
+/* The halo exchange plan of rank `rank` (new; the reference has no distributed path): the
+ * byte ranges a slab's exchange of `depth` rows of `nfields` level-stacked fields moves.
+ * Offsets are relative to a field's row 0 of level 0 in the slab-grid layout (`pitch`
+ * elements per row, `level_stride` elements per level, 12 halo rows above and below each
+ * level). Per neighbour there is ONE message: its send segments (kind 0) concatenated in
+ * plan order (field-major, then level; msg_offset = position in the message), received
+ * into the receive segments (kind 1) in the same order. ws_sim_create_slab's RCCL exchange
+ * and ws_group_run's device copies both execute exactly this plan (pack, move, unpack).
+ * out = NULL: only count / pitch / level_stride. */
+typedef struct {
+    int32_t peer;        /* neighbour rank */
+    int32_t kind;        /* 0 = send, 1 = receive */
+    int32_t field;       /* index into the exchanged fields (u, v, h: 0, 1, 2) */
+    int32_t level;
+    int64_t offset;      /* bytes from the field's row 0 of level 0 */
+    int64_t bytes;
+    int64_t msg_offset;  /* bytes into the message exchanged with `peer` */
+} ws_xfer_t;
+int ws_slab_exchange_plan(int32_t width, int32_t rows, int32_t levels, int32_t dtype, int32_t rank, int32_t nranks,
+                          int32_t nfields, int32_t depth, ws_xfer_t* out, int32_t capacity, int32_t* count,
+                          int64_t* pitch, int64_t* level_stride);
+
 /* Row range [row0, row0 + rows) of rank `rank` in the balanced split of `height` rows. */
 int ws_slab_partition(int32_t height, int32_t rank, int32_t nranks, int32_t* row0, int32_t* rows);
 /* Collectives on the slab communicator (max over ranks of one double; barrier). On a
@@ -290,16 +312,33 @@ int ws_sim_set_kernel_timing(ws_sim_t* sim, int32_t enable);
 int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, double* total_ms,
                          double* bytes_per_launch);
 
-/* The fused step-kernel variant in use: kernel 0 = LDS workgroups, 1 = DPP waves (64
- * columns per wave), 2 = column pairs (128 columns per wave), 3 = DPP waves with y rows
- * staged through LDS by LDS-DMA, 4 = the same with y rows read from LDS in place (three
- * waves per SIMD), 5 = column pairs with y rows read from LDS in place, -1 = per-stage
- * kernels;
- * seg_rows = output rows per segment, out_cols = output columns per strip (a multiple of
- * the 128-byte line when the strips are line-aligned). Chosen by timing every variant on
- * the real grid at the first run (all are bit-identical), unless WS_KERNEL / WS_SEG_ROWS /
- * WS_ALIGN fix it. */
+/* The fused step-kernel variant in use: kernel 0 = LDS workgroups (256 columns), 4 = DPP
+ * waves (64 columns per wave) with y rows staged by LDS-DMA and read from LDS in place,
+ * 5 = the same with an adjacent column pair per lane (128 columns per wave), -1 = per-stage
+ * kernels (ids 1-3 are retired variants); seg_rows = output rows per segment, out_cols =
+ * output columns per strip (a multiple of the 128-byte line when the strips are
+ * line-aligned). Chosen by timing every variant on the real grid at the first run (all give
+ * identical results), unless WS_KERNEL / WS_SEG_ROWS / WS_ALIGN fix it. The choice is
+ * cached per process by (grid shape, levels, precision, integrator, numerics, slab
+ * position), and a slab decomposition uses rank 0's choice on every rank. */
 int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols);
+
+/* ---- numerics mode of the fused step kernels ------------------------------------------
+ * WS_NUMERICS_EXACT: the reference's arithmetic in the reference's evaluation order, no
+ *   contraction: bit-for-bit equal to the CPU solver (weather_simulation.cpp:160-540).
+ * WS_NUMERICS_FAST: the same tendencies and integrators re-associated for the hardware
+ *   (fused multiply-adds, the 1/(2dx) factor folded into the update constants, RK4's final
+ *   combination as y + dt/3 ((k2 + k3) + k4)); isotropic spacing only (dx == dy: otherwise
+ *   the kernels stay exact). Results differ from the reference by rounding only
+ *   (north_star tolerance for fp64: <= 1e-10 relative L2; measured in
+ *   tests/test_gpu_numerics.py).
+ * Default: FAST for fp64 simulations, EXACT for fp32; the environment variable
+ * WS_NUMERICS=exact|fast overrides the default at creation. The per-stage fallback kernels
+ * (WS_FUSED=0) and the adapter / raw-launcher entry points are always exact. */
+#define WS_NUMERICS_EXACT 0
+#define WS_NUMERICS_FAST 1
+int ws_sim_set_numerics(ws_sim_t* sim, int32_t mode);
+int ws_sim_get_numerics(const ws_sim_t* sim, int32_t* mode);
 
 #ifdef __cplusplus
 }

@@ -35,7 +35,7 @@ SlabComm::SlabComm(int rank, int nranks, const uint8_t* id128) : rank_(rank), nr
     ncclComm_t c = nullptr;
     check(ncclCommInitRank(&c, nranks, id, rank), "ncclCommInitRank");
     comm_ = c;
-    hcheck(hipMalloc(&scratch_, sizeof(double)), "hipMalloc");
+    hcheck(hipMalloc(&scratch_, 16 * sizeof(double)), "hipMalloc");
 }
 
 SlabComm::~SlabComm() {
@@ -45,27 +45,34 @@ SlabComm::~SlabComm() {
 
 void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream) {
     if (nranks_ == 1) return;
+    if (nfields > kMaxHaloFields) throw CommError("too many fields for one exchange");
+    const HaloPlan plan = make_halo_plan(g, elem_size, rank_, nranks_, nfields, depth);
+    staging_.ensure(plan.msg_bytes());
+    HaloFields hf{};
+    for (int f = 0; f < nfields; ++f) hf.f[f] = (char*)fields[f];
+    for (int side = 0; side < 2; ++side)
+        if (plan.has[side]) hcheck(halo_pack(plan, hf, side, staging_.send[side], stream), "halo_pack");
     const ncclComm_t c = (ncclComm_t)comm_;
-    const size_t row_bytes = (size_t)g.pitch * elem_size;
-    const size_t bytes = row_bytes * depth;
-    const size_t lbytes = (size_t)g.lstride * elem_size;
+    const size_t bytes = (size_t)plan.msg_bytes();
     check(ncclGroupStart(), "ncclGroupStart");
-    for (int f = 0; f < nfields; ++f) {
-        char* base = (char*)fields[f];
-        for (int l = 0; l < g.L; ++l) {
-            char* lv = base + (size_t)l * lbytes;
-            if (rank_ > 0) {  // my top rows <-> upper neighbour's bottom rows
-                check(ncclSend(lv, bytes, ncclChar, rank_ - 1, c, stream), "ncclSend");
-                check(ncclRecv(lv - bytes, bytes, ncclChar, rank_ - 1, c, stream), "ncclRecv");
-            }
-            if (rank_ < nranks_ - 1) {
-                check(ncclSend(lv + (size_t)(g.H - depth) * row_bytes, bytes, ncclChar, rank_ + 1, c, stream),
-                      "ncclSend");
-                check(ncclRecv(lv + (size_t)g.H * row_bytes, bytes, ncclChar, rank_ + 1, c, stream), "ncclRecv");
-            }
-        }
+    for (int side = 0; side < 2; ++side) {
+        if (!plan.has[side]) continue;
+        check(ncclSend(staging_.send[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclSend");
+        check(ncclRecv(staging_.recv[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclRecv");
     }
     check(ncclGroupEnd(), "ncclGroupEnd");
+    for (int side = 0; side < 2; ++side)
+        if (plan.has[side]) hcheck(halo_unpack(plan, hf, side, staging_.recv[side], stream), "halo_unpack");
+}
+
+void SlabComm::broadcast_i32(int32_t* v, int n, int root, hipStream_t stream) {
+    if (nranks_ == 1 || n <= 0) return;
+    if (n > 16) throw CommError("broadcast_i32: at most 16 values");
+    int32_t* d = (int32_t*)scratch_;  // scratch_ holds 16 doubles = 32 int32
+    hcheck(hipMemcpyAsync(d, v, n * sizeof(int32_t), hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    check(ncclBroadcast(d, d, n, ncclInt32, root, (ncclComm_t)comm_, stream), "ncclBroadcast");
+    hcheck(hipMemcpyAsync(v, d, n * sizeof(int32_t), hipMemcpyDeviceToHost, stream), "hipMemcpyAsync");
+    hcheck(hipStreamSynchronize(stream), "hipStreamSynchronize");
 }
 
 double SlabComm::allreduce_max(double v, hipStream_t stream) {

@@ -1,10 +1,5 @@
-// y-slab halo exchange over RCCL (ncclSend / ncclRecv between neighbouring ranks).
-//
-// The reference has no distributed path; this is new. Rank r owns rows
-// [row0, row0 + H) of the global grid. Its `depth` top rows go to rank r-1 (which stores
-// them as rows [H', H'+depth) of its own buffers) and its `depth` bottom rows go to rank
-// r+1 (stored as rows [-depth, 0)). The global top / bottom edges keep the reference's
-// clamp-to-self stencil (Geom::top_clamp / bot_clamp), so no exchange happens there.
+// y-slab halo exchange over RCCL between the processes of a slab decomposition: the plan
+// of ws_halo.h (one packed message per neighbour), moved with ncclSend / ncclRecv.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -12,6 +7,7 @@
 #include <cstdint>
 #include <stdexcept>
 
+#include "ws_halo.h"
 #include "ws_internal.h"
 
 namespace ws {
@@ -39,8 +35,11 @@ public:
     int nranks() const { return nranks_; }
 
     // Exchange `depth` halo rows of `nfields` level-stacked fields (row 0 of level 0 at
-    // fields[i]) with both neighbours, enqueued on `stream` as one grouped RCCL call.
+    // fields[i]) with both neighbours, enqueued on `stream`: pack each neighbour's segments
+    // into one message (halo_pack), one grouped RCCL send / recv per neighbour, unpack.
     void exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream);
+    // rank `root`'s n int32 values to every rank (host in, host out; synchronises `stream`)
+    void broadcast_i32(int32_t* v, int n, int root, hipStream_t stream);
     // In-place max over ranks of one double (device scratch owned by the comm).
     double allreduce_max(double v, hipStream_t stream);
     void barrier(hipStream_t stream);
@@ -49,6 +48,7 @@ private:
     int rank_ = 0, nranks_ = 1;
     void* comm_ = nullptr;  // ncclComm_t
     double* scratch_ = nullptr;
+    HaloStaging staging_;
 };
 
 }  // namespace ws

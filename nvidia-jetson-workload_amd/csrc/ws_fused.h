@@ -13,7 +13,7 @@ struct FusedArgs {
     T *out_u, *out_v, *out_h;     // y_{n+1}
     T c_half;                     // 0.5f * dt
     T c_dt;                       // dt
-    T c_dt6;                      // dt / 6.0f
+    T c_dt6;                      // dt / 6.0f (fast numerics: dt / 3 * s, see prepare_fast)
     T gravity, coriolis_f;
     Spacing<T> sp1;               // stage 1: spacing of the current grid
     Spacing<T> sp2;               // later stages: spacing of the temp grid (= config)
@@ -27,45 +27,44 @@ struct FusedArgs {
     int32_t ga_y0, ga_y1, ga_n;
     int32_t gb_y0, gb_y1;
     int32_t seg_n;
-    // 1 = "scaled tendencies" (set by scale_tendencies, below): the kernels leave the
-    // central differences unscaled and every constant that multiplies them carries the
-    // 1/(2 dx) factor instead; 0 = the kernels divide by (2 dx) as the reference writes it
-    int32_t scaled;
+    // spacing / numerics mode of the launch (SpacingMode below), set by the host
+    int32_t sp_mode;
 };
 
-// Scaled tendencies. When 2dx = 2dy = 2^-k for both spacings (s = 1/(2dx) = 2^k), every
-// tendency the reference computes is s times the same expression evaluated on the raw
-// differences D = (ar - al): multiplying by a power of two commutes with IEEE rounding, so
-//   (-u)*(s*D) = s*round((-u)*D),   g*(s*D) = s*round(g*D),   s*A - s*B = s*round(A - B),
-//   f*v = s*round((f/s)*v),   y + c*(s*K) = y + round((c*s)*K),   s*a + 2*(s*b) = s*round(a + 2*b),
-// with f/s and c*s exact. The kernels evaluate K = k/s (g unchanged, f -> f/s) and the
-// update constants carry s, skipping the 6 multiplications by s per stage (RK4: 24 of ~170
-// fp64 ops per cell). Results are bit-identical to the reference's
-// evaluation order whenever no intermediate is subnormal (|x| < 2^-1022 fp64, 2^-126 fp32)
-// or within a factor 2^|k| of overflow. Subnormal intermediates do occur (the reference
-// fixture "mountain" fp32 after 50 steps: values ~1e-42 ahead of the wave front differ in
-// their last subnormal bits), so this is OPT-IN (WS_SCALED=1): the default is bit-exact.
-// Spacing modes of the fused kernels (template parameter): divide as the reference writes
-// it; multiply by the exact reciprocal (2dx, 2dy powers of two: bit-identical); scaled.
-enum SpacingMode : int { kSpDiv = 0, kSpMul = 1, kSpScaled = 2 };
+// Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).
+//  * kSpDiv: the central difference (ar - al) / (2 dx) divides, as the reference writes it;
+//  * kSpMul: multiplies by the exact reciprocal (2dx, 2dy powers of two) -- bit-identical;
+//  * kSpFast / kSpFast0 ("fast numerics", fp64 tolerance mode): the reference's tendencies
+//    re-associated for the hardware. With s = 1 / (2 dx) = 1 / (2 dy) (isotropic spacing,
+//    any value) every tendency is s times the same expression on the raw differences
+//    D = ar - al, so the kernel evaluates K = k / s with fused multiply-adds (f -> f / s)
+//    and the update constants carry s; RK4-as-implemented's final combination
+//    y + dt/6 (((k4 + 2 k2) + 2 k3) + k4) is evaluated as y + (dt/3)((k2 + k3) + k4).
+//    kSpFast0 drops the Coriolis terms (f == 0). Not bit-identical: every result differs
+//    from the reference by rounding only (fp64: <= 1e-10 relative L2 is the north_star
+//    tolerance; tests/test_gpu_numerics.py measures it), and about half the fp64 VALU work
+//    of the exact evaluation order.
+enum SpacingMode : int { kSpDiv = 0, kSpMul = 1, kSpFast = 2, kSpFast0 = 3 };
+
 template <typename T>
-inline int fused_sp_mode(const FusedArgs<T>& a) {
-    if (a.scaled) return kSpScaled;
+inline int exact_sp_mode(const FusedArgs<T>& a) {
     return a.sp1.pow2x && a.sp1.pow2y && a.sp2.pow2x && a.sp2.pow2y ? kSpMul : kSpDiv;
 }
 
+// Set up a launch's constants for fast numerics when the spacing allows it (isotropic, and
+// the same on both grids); otherwise leave the exact mode. Returns the mode chosen.
 template <typename T>
-inline void scale_tendencies(FusedArgs<T>& a) {
+inline int prepare_fast(FusedArgs<T>& a) {
     const Spacing<T>& p = a.sp1;
     const Spacing<T>& q = a.sp2;
-    a.scaled = p.pow2x && p.pow2y && q.pow2x && q.pow2y && p.inv2dx == p.inv2dy && q.inv2dx == q.inv2dy &&
-               p.inv2dx == q.inv2dx;
-    if (!a.scaled) return;
-    const T s = p.inv2dx;
+    if (!(p.two_dx == p.two_dy && q.two_dx == q.two_dy && p.two_dx == q.two_dx)) return a.sp_mode = exact_sp_mode(a);
+    const T s = T(1) / p.two_dx;
+    const T dt = a.c_dt;
     a.c_half *= s;
-    a.c_dt *= s;
-    a.c_dt6 *= s;
+    a.c_dt = dt * s;
+    a.c_dt6 = dt / T(3) * s;  // fast mode: the final combination's dt/3
     a.coriolis_f /= s;
+    return a.sp_mode = a.coriolis_f == T(0) ? kSpFast0 : kSpFast;
 }
 
 template <typename T>
@@ -79,43 +78,33 @@ __host__ __device__ inline void fused_rows(const FusedArgs<T>& a, int i, int& y0
     }
 }
 
-// nstages: 1 (Euler), 2 (RK2 midpoint), 4 (RK4-as-implemented)
-// LDS variant: 256-lane workgroups, horizontal neighbours through LDS, one barrier per row.
+// nstages: 1 (Euler), 2 (RK2 midpoint), 4 (RK4-as-implemented). Three variants, all giving
+// identical results (the autotuner picks one per grid, ws_runtime.cpp):
+// "lds": 256-lane workgroups, horizontal neighbours through LDS, one barrier per row.
 template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
-// DPP variant: independent 64-lane waves, horizontal neighbours by DPP lane shifts.
+// "dppy": independent 64-lane waves, one column per lane, horizontal neighbours by DPP lane
+// shifts, y rows staged by LDS-DMA and read from LDS in place.
 constexpr int kDppCols = 64;
-// y rows: loaded into a VGPR ring (kDppVgpr), staged through LDS by LDS-DMA (16 B per lane)
-// and copied to the VGPR ring (kDppDma), or LDS-DMA staged and read from LDS in place
-// (kDppLdsY: fewer VGPRs, three waves per SIMD)
-enum DppMode : int { kDppVgpr = 0, kDppDma = 1, kDppLdsY = 2 };
 template <typename T>
-hipError_t launch_fused_step_dpp(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int mode);
-// the three modes' launchers (one translation unit each)
+hipError_t launch_fused_step_dppy(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+// "x2y": as dppy with an adjacent column pair per lane (128-column strips).
 template <typename T>
-hipError_t launch_dpp_vgpr(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
-template <typename T>
-hipError_t launch_dpp_dma(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
-template <typename T>
-hipError_t launch_dpp_ldsy(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
-// Strip geometry, per variant: columns per strip and the left margin (the dependency cone;
-// the x2 variant rounds it up to whole column pairs). The output window of strip s is
-// [s * out_w, (s + 1) * out_w); out_w is at most columns - 2 * margin, and when `aligned`
-// it is rounded down to whole 128-byte lines so no two strips write parts of one line.
-enum FusedVariant : int { kFusedLds = 0, kFusedDpp = 1, kFusedX2 = 2, kFusedDppDma = 3, kFusedDppLdsY = 4,
-                          kFusedX2Y = 5 };
-inline int fused_strip_cols(int variant) {
-    return variant == kFusedX2 || variant == kFusedX2Y ? 128
-           : (variant == kFusedDpp || variant == kFusedDppDma || variant == kFusedDppLdsY) ? 64
-                                                                                             : 256;
-}
-// (the DMA variant rounds it up to whole 16-byte chunks: a strip's LDS-DMA chunks then
+// Strip geometry, per variant: columns per strip and the left margin (the dependency cone,
+// rounded up to whole 16-byte DMA chunks for the LDS-DMA variants: a strip's chunks then
 // never straddle column 0, where a partly negative chunk would be dropped whole by the
-// buffer range check)
+// buffer range check). The output window of strip s is [s * out_w, (s + 1) * out_w); out_w
+// is at most columns - 2 * margin, and when `aligned` it is rounded down to whole 128-byte
+// lines so no two strips write parts of one line. (Variant ids are ABI values,
+// ws_sim_fused_variant; 1-3 belonged to variants removed after never winning a config.)
+enum FusedVariant : int { kFusedLds = 0, kFusedDppLdsY = 4, kFusedX2Y = 5 };
+inline int fused_strip_cols(int variant) {
+    return variant == kFusedX2Y ? 128 : variant == kFusedDppLdsY ? 64 : 256;
+}
 inline int fused_margin(int variant, int nstages, int elem_bytes) {
-    if (variant == kFusedX2) return (nstages + 1) / 2 * 2;
-    if (variant == kFusedDppDma || variant == kFusedDppLdsY || variant == kFusedX2Y) {
+    if (variant == kFusedDppLdsY || variant == kFusedX2Y) {
         const int g = 16 / elem_bytes;
         return (nstages + g - 1) / g * g;
     }
@@ -126,12 +115,5 @@ inline int fused_out_w(int variant, int nstages, int elem_bytes, bool aligned) {
     const int line = 128 / elem_bytes;
     return aligned && w >= line ? w / line * line : w;
 }
-
-// x2 variant: independent 64-lane waves, two adjacent columns per lane (128-column strips).
-template <typename T>
-hipError_t launch_fused_step_x2(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
-// x2y variant: column pairs with y rows staged by LDS-DMA and read from LDS in place
-template <typename T>
-hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
 }  // namespace ws

@@ -56,7 +56,7 @@ __device__ __forceinline__ void publish(T* colp, const V3<T>& v) {
 // j+1 (down) and the published row j (x-neighbours, quantity Q). YCLAMP: the segment
 // touches a global y edge, where the reference clamps j-1 / j+1 to j
 // (weather_simulation.cpp:512-513).
-template <int POW2, bool YCLAMP, int NST, int Q, typename T>
+template <int MODE, bool YCLAMP, int NST, int Q, typename T>
 __device__ __forceinline__ V3<T> stage_tend(const T* lcol, int j, const Geom& g, const V3<T>& up, const V3<T>& mid,
                                             const V3<T>& down, const Spacing<T>& sp, T grav, T cor) {
     constexpr int kCs = Lds<T, NST>::kCs;
@@ -69,9 +69,9 @@ __device__ __forceinline__ V3<T> stage_tend(const T* lcol, int j, const Geom& g,
         // select by value (a ?: on two lvalues selects an address and spills to scratch)
         const V3<T> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
         const V3<T> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
-        return tend<POW2>(mid, l, r, t, b, sp, grav, cor);
+        return tend<MODE>(mid, l, r, t, b, sp, grav, cor);
     } else {
-        return tend<POW2>(mid, l, r, up, down, sp, grav, cor);
+        return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
     }
 }
 
@@ -82,7 +82,7 @@ constexpr int kU = 8;   // march unroll = y ring length
 #define WS_FUSED_MINW 1
 #endif
 
-template <typename T, int NST, int POW2>
+template <typename T, int NST, int MODE>
 __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(FusedArgs<T> a, Geom g) {
     // All per-lane state lives in rotating register rings indexed by the march phase P
     // (compile-time): the body is instantiated for P = 0..kU-1, so ring "shifts" are renames,
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
     const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
     const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
 
-    // buffer addressing as in ws_fused_dpp.hip: per-field descriptors based at this
+    // buffer addressing as in ws_fused_dppy.hip: per-field descriptors based at this
     // workgroup's first row, row = scalar offset, column = fixed voffset; stores of
     // non-output lanes / rows go to an out-of-range voffset and are dropped (no branch)
     const int64_t lofs = (int64_t)blockIdx.z * g.lstride;
@@ -190,47 +190,40 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
 
         if constexpr (on(1)) {
             // stage 1 at row R-1 from y rows R-2, R-1, R
-            const V3<T> k1 = stage_tend<POW2, YC, NST, 0 + prv>(lcol, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)],
+            const V3<T> k1 = stage_tend<MODE, YC, NST, 0 + prv>(lcol, R - 1, g, Y[yi(-2)], Y[yi(-1)], Y[yi(0)],
                                                                 a.sp1, a.gravity, a.coriolis_f);
             if constexpr (NST == 1) {
-                store_row(R - 1, axpy(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
+                store_row(R - 1, axpy<MODE>(Y[yi(-1)], a.c_dt, k1));  // Euler: y + dt k
             } else {
-                const V3<T> s1 = axpy(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
+                const V3<T> s1 = axpy<MODE>(Y[yi(-1)], a.c_half, k1);  // y + (0.5f dt) k
                 if constexpr (on(2)) {
                     // stage 2 at row R-2 from s1 rows R-3, R-2, R-1
-                    const V3<T> k2 = stage_tend<POW2, YC, NST, 2 + prv>(lcol, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1,
+                    const V3<T> k2 = stage_tend<MODE, YC, NST, 2 + prv>(lcol, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1,
                                                                         a.sp2, a.gravity, a.coriolis_f);
                     if constexpr (NST == 2) {
-                        store_row(R - 2, axpy(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
+                        store_row(R - 2, axpy<MODE>(Y[yi(-2)], a.c_dt, k2));  // RK2: y + dt k2
                     } else {
-                        const V3<T> s2 = axpy(Y[yi(-2)], a.c_half, k2);
+                        const V3<T> s2 = axpy<MODE>(Y[yi(-2)], a.c_half, k2);
                         if constexpr (on(3)) {
                             // stage 3 at row R-3
-                            const V3<T> k3 = stage_tend<POW2, YC, NST, 4 + prv>(lcol, R - 3, g, S2[r2(-4)],
+                            const V3<T> k3 = stage_tend<MODE, YC, NST, 4 + prv>(lcol, R - 3, g, S2[r2(-4)],
                                                                                 S2[r2(-3)], s2, a.sp2, a.gravity,
                                                                                 a.coriolis_f);
-                            const V3<T> s3 = axpy(Y[yi(-3)], a.c_dt, k3);
+                            const V3<T> s3 = axpy<MODE>(Y[yi(-3)], a.c_dt, k3);
                             if constexpr (on(4)) {
                                 // stage 4 at row R-4
-                                const V3<T> k4 = stage_tend<POW2, YC, NST, 6 + prv>(lcol, R - 4, g, S3[r2(-5)],
+                                const V3<T> k4 = stage_tend<MODE, YC, NST, 6 + prv>(lcol, R - 4, g, S3[r2(-5)],
                                                                                     S3[r2(-4)], s3, a.sp2,
                                                                                     a.gravity, a.coriolis_f);
                                 // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
-                                const T two = T(2);
-                                const V3<T>& y4 = Y[yi(-4)];
-                                const V3<T>& kk2 = K2[r2(-4)];
-                                const V3<T>& kk3 = K3[r2(-4)];
-                                V3<T> o;
-                                o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
-                                o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
-                                o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                                const V3<T> o = rk4_final<MODE>(Y[yi(-4)], a.c_dt6, k4, K2[r2(-4)], K3[r2(-4)]);
                                 store_row(R - 4, o);
                             } else {
                                 store_row(y0 - 1, Z);
                             }
                             pub(Q3c{}, s3);
                             S3[r2(-3)] = s3;
-                            K3[r2(-3)] = k3;
+                            K3[r2(-3)] = rk4_keep3<MODE>(K2[r2(-3)], k3);
                         } else {
                             store_row(y0 - 1, Z);
                         }
@@ -286,18 +279,20 @@ hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, 
         return hipErrorInvalidValue;
     const dim3 grid((g.W + out_w - 1) / out_w, a.seg_n, g.L);
     const dim3 block(kFusedCols);
-    const int sp_mode = fused_sp_mode(a);  // spacing mode (ws_fused.h)
-#define WS_FUSED_LAUNCH(N)                                                                               \
-    if (sp_mode == kSpScaled) hipLaunchKernelGGL((fused_step_kernel<T, N, kSpScaled>), grid, block, 0, s, a, g); \
-    else if (sp_mode == kSpMul) hipLaunchKernelGGL((fused_step_kernel<T, N, kSpMul>), grid, block, 0, s, a, g); \
-    else hipLaunchKernelGGL((fused_step_kernel<T, N, kSpDiv>), grid, block, 0, s, a, g);
+#define WS_FUSED_GO(N, M) hipLaunchKernelGGL((fused_step_kernel<T, N, M>), grid, block, 0, s, a, g)
+#define WS_FUSED_G1(M) WS_FUSED_GO(1, M)
+#define WS_FUSED_G2(M) WS_FUSED_GO(2, M)
+#define WS_FUSED_G4(M) WS_FUSED_GO(4, M)
     switch (nstages) {
-        case 1: WS_FUSED_LAUNCH(1) break;
-        case 2: WS_FUSED_LAUNCH(2) break;
-        case 4: WS_FUSED_LAUNCH(4) break;
+        case 1: WS_SP_DISPATCH(a.sp_mode, WS_FUSED_G1) break;
+        case 2: WS_SP_DISPATCH(a.sp_mode, WS_FUSED_G2) break;
+        case 4: WS_SP_DISPATCH(a.sp_mode, WS_FUSED_G4) break;
         default: return hipErrorInvalidValue;
     }
-#undef WS_FUSED_LAUNCH
+#undef WS_FUSED_G1
+#undef WS_FUSED_G2
+#undef WS_FUSED_G4
+#undef WS_FUSED_GO
     return hipGetLastError();
 }
 

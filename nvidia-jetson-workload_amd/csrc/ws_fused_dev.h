@@ -1,6 +1,6 @@
-// Device helpers shared by the wave-independent fused step kernels (ws_fused_dpp.hip,
-// ws_fused_x2.hip): buffer-descriptor memory access, DPP lane shifts, and the SWE
-// tendency written once for scalar and 2-wide (ext_vector) cell values.
+// Device helpers shared by the fused step kernels (ws_fused.hip, ws_fused_dppy.hip,
+// ws_fused_x2y.hip): buffer-descriptor memory access, DPP lane shifts, and the SWE tendency
+// written once for scalar and 2-wide (ext_vector) cell values, per spacing / numerics mode.
 #pragma once
 
 #include "ws_fused.h"
@@ -91,36 +91,93 @@ struct V3 {
     VT u, v, h;
 };
 
-// Central difference, per spacing mode (ws_fused.h, fused_sp_mode): the reference's
-// (ar - al) / (2.0f * d); the same times the exact reciprocal when 2d is a power of two;
-// or, for scaled tendencies, the raw difference (the 1/(2d) factor rides on the constants).
+// Central difference, per spacing mode (ws_fused.h): the reference's (ar - al) / (2.0f * d);
+// the same times the exact reciprocal when 2d is a power of two; or, for fast numerics, the
+// raw difference (the 1/(2d) factor rides on the constants).
 template <int MODE, typename VT, typename T>
 __device__ __forceinline__ VT cdiff(VT ar, VT al, T two_d, T inv) {
-    if constexpr (MODE == kSpScaled) return ar - al;
+    if constexpr (MODE >= kSpFast) return ar - al;
     else if constexpr (MODE == kSpMul) return (ar - al) * inv;  // exact: inv is a power of two
     else return (ar - al) / two_d;
 }
 
-template <int POW2, typename VT, typename T>
+// fused multiply-add a * b + c, element-wise for ext_vector values (one rounding)
+template <typename VT>
+__device__ __forceinline__ VT fmadd(VT a, VT b, VT c) {
+    return __builtin_elementwise_fma(a, b, c);
+}
+
+template <int MODE, typename VT, typename T>
 __device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V3<VT>& r, const V3<VT>& t,
                                        const V3<VT>& b, const Spacing<T>& sp, T g, T f) {
-    const VT u_x = cdiff<POW2>(r.u, l.u, sp.two_dx, sp.inv2dx);
-    const VT u_y = cdiff<POW2>(b.u, t.u, sp.two_dy, sp.inv2dy);
-    const VT v_x = cdiff<POW2>(r.v, l.v, sp.two_dx, sp.inv2dx);
-    const VT v_y = cdiff<POW2>(b.v, t.v, sp.two_dy, sp.inv2dy);
-    const VT h_x = cdiff<POW2>(r.h, l.h, sp.two_dx, sp.inv2dx);
-    const VT h_y = cdiff<POW2>(b.h, t.h, sp.two_dy, sp.inv2dy);
+    const VT u_x = cdiff<MODE>(r.u, l.u, sp.two_dx, sp.inv2dx);
+    const VT u_y = cdiff<MODE>(b.u, t.u, sp.two_dy, sp.inv2dy);
+    const VT v_x = cdiff<MODE>(r.v, l.v, sp.two_dx, sp.inv2dx);
+    const VT v_y = cdiff<MODE>(b.v, t.v, sp.two_dy, sp.inv2dy);
+    const VT h_x = cdiff<MODE>(r.h, l.h, sp.two_dx, sp.inv2dx);
+    const VT h_y = cdiff<MODE>(b.h, t.h, sp.two_dy, sp.inv2dy);
     V3<VT> k;
-    k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
-    k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
-    k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
+    if constexpr (MODE >= kSpFast) {
+        // fast numerics: k / s = -u D_x u - v D_y u - g D_x h + (f / s) v, ... (ws_fused.h)
+        const VT ng = (VT)(-g);
+        k.u = fmadd(-c.v, u_y, fmadd(ng, h_x, -c.u * u_x));
+        k.v = fmadd(-c.v, v_y, fmadd(ng, h_y, -c.u * v_x));
+        k.h = fmadd(-c.v, h_y, fmadd(-c.u, h_x, -c.h * (u_x + v_y)));
+        if constexpr (MODE == kSpFast) {
+            k.u = fmadd((VT)f, c.v, k.u);
+            k.v = fmadd((VT)(-f), c.u, k.v);
+        }
+    } else {
+        // the reference's order (weather_simulation.cpp:535-537); no contraction in this build
+        k.u = -c.u * u_x - c.v * u_y - g * h_x + f * c.v;
+        k.v = -c.u * v_x - c.v * v_y - g * h_y - f * c.u;
+        k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
+    }
     return k;
 }
 
-template <typename VT, typename T>
+// stage update y + c k (fast numerics: one fused multiply-add)
+template <int MODE, typename VT, typename T>
 __device__ __forceinline__ V3<VT> axpy(const V3<VT>& y, T c, const V3<VT>& k) {
-    return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
+    if constexpr (MODE >= kSpFast) return {fmadd((VT)c, k.u, y.u), fmadd((VT)c, k.v, y.v), fmadd((VT)c, k.h, y.h)};
+    else return {y.u + c * k.u, y.v + c * k.v, y.h + c * k.h};
 }
+
+// RK4-as-implemented: what the stage-3 ring keeps for the final combination -- k3 (exact), or
+// the running sum k2 + k3 (fast numerics)
+template <int MODE, typename VT>
+__device__ __forceinline__ V3<VT> rk4_keep3(const V3<VT>& k2, const V3<VT>& k3) {
+    if constexpr (MODE >= kSpFast) return {k2.u + k3.u, k2.v + k3.v, k2.h + k3.h};
+    else return k3;
+}
+
+// The final combination (k1 aliases k4, weather_simulation.cpp:437-451):
+// exact: y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4); fast: y + dt/3 * (kept + k4), kept = k2 + k3
+// (c = a.c_dt6, which prepare_fast turns into dt/3 * s)
+template <int MODE, typename VT, typename T>
+__device__ __forceinline__ V3<VT> rk4_final(const V3<VT>& y, T c, const V3<VT>& k4, const V3<VT>& k2,
+                                            const V3<VT>& kept3) {
+    if constexpr (MODE >= kSpFast) {
+        const VT cv = (VT)c;
+        return {fmadd(cv, kept3.u + k4.u, y.u), fmadd(cv, kept3.v + k4.v, y.v), fmadd(cv, kept3.h + k4.h, y.h)};
+    } else {
+        const T two = T(2);
+        V3<VT> o;
+        o.u = y.u + c * (((k4.u + two * k2.u) + two * kept3.u) + k4.u);
+        o.v = y.v + c * (((k4.v + two * k2.v) + two * kept3.v) + k4.v);
+        o.h = y.h + c * (((k4.h + two * k2.h) + two * kept3.h) + k4.h);
+        return o;
+    }
+}
+
+// launch a fused kernel template instantiated per spacing mode: GO(MODE) for the runtime mode
+#define WS_SP_DISPATCH(mode, GO)           \
+    switch (mode) {                        \
+        case kSpFast0: GO(kSpFast0); break; \
+        case kSpFast: GO(kSpFast); break;   \
+        case kSpMul: GO(kSpMul); break;     \
+        default: GO(kSpDiv); break;         \
+    }
 
 // XCD-aware work mapping: consecutive work items (neighbouring strips of one segment,
 // which share halo columns) go to blocks b, b+8, ... that the dispatcher places on the

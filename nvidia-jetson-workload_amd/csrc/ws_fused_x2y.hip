@@ -1,8 +1,8 @@
 // Fused multi-stage time step: column pairs per lane with LDS-resident y rows ("x2y").
 //
-// The march of ws_fused_dpp.hip's LDS-resident-y mode (one kernel per time step; y read
+// The march of ws_fused_dppy.hip (one kernel per time step; y read
 // once, y' written once; stage s = 1..NST computes row R - s while row R arrives) with the
-// lane layout of ws_fused_x2.hip: each lane owns an adjacent column pair, a 64-lane wave a
+// column-pair lane layout: each lane owns an adjacent column pair, a 64-lane wave a
 // 128-column strip, so of a pair's four horizontal neighbours two are the lane's own values
 // (half the DPP moves per cell) and the strip overlap is 2 * 4 of 128 columns (RK4: 6 %
 // recomputed instead of 12.5 %). The y rows arrive by LDS-DMA (buffer_load_dwordx4 ... lds,
@@ -11,9 +11,9 @@
 // store per field and row (a pair never straddles the row's end: pitch is a multiple of 64
 // elements, so the column after an odd W is row padding, whose content is unspecified).
 //
-// Arithmetic per cell is the reference's, in the reference's order
-// (weather_simulation.cpp:160-455, 473-540), element-wise on the pair: results are
-// bit-for-bit those of the CPU solver.
+// Arithmetic per cell, element-wise on the pair: the reference's, in the reference's order
+// (weather_simulation.cpp:160-455, 473-540) -- bit-for-bit those of the CPU solver -- or
+// fast numerics (ws_fused.h), by spacing mode.
 #include <type_traits>
 #include <utility>
 
@@ -44,7 +44,7 @@ struct EdgeCols {
 
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage; the
 // reference's clamp-to-self at global edges (weather_simulation.cpp:510-513).
-template <int POW2, bool XCLAMP, bool YCLAMP, typename T>
+template <int MODE, bool XCLAMP, bool YCLAMP, typename T>
 __device__ __forceinline__ V3<P2<T>> stage_tend(const EdgeCols& e, int j, const Geom& g, const V3<P2<T>>& up,
                                                 const V3<P2<T>>& mid, const V3<P2<T>>& down, const Spacing<T>& sp,
                                                 T grav, T cor) {
@@ -62,9 +62,9 @@ __device__ __forceinline__ V3<P2<T>> stage_tend(const EdgeCols& e, int j, const 
         const bool ybot = (j == g.H - 1) && g.bot_clamp;
         const V3<VT> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
         const V3<VT> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
-        return tend<POW2>(mid, l, r, t, b, sp, grav, cor);
+        return tend<MODE>(mid, l, r, t, b, sp, grav, cor);
     } else {
-        return tend<POW2>(mid, l, r, up, down, sp, grav, cor);
+        return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
     }
 }
 
@@ -74,8 +74,8 @@ constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 
 #define WS_X2Y_MINW 1
 #endif
 
-template <typename T, int NST, int POW2>
-__global__ __launch_bounds__(kWave, WS_X2Y_MINW) void fused_x2y_kernel(FusedArgs<T> a, Geom g, int nstrips,
+template <typename T, int NST, int MODE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(WS_X2Y_MINW))) void fused_x2y_kernel(FusedArgs<T> a, Geom g, int nstrips,
                                                                         int nsegs) {
     using VT = P2<T>;
     constexpr int kG = 16 / (2 * (int)sizeof(T));  // rows per DMA instruction (fp64 1, fp32 2)
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kWave, WS_X2Y_MINW) void fused_x2y_kernel(FusedArgs
     // wait until at most the younger DMA loads are outstanding (the DMAs issued since the
     // group, incl. the reading body's): loads complete in order, stores do not (a younger
     // store can retire before an older load), so stores are not counted -- see
-    // ws_fused_dpp_kernel.h
+    // ws_fused_dppy.hip
     constexpr int kWaitN = 3 * (kD / kG);
     constexpr int kM = margin<T>(NST);
     const int out_w = a.out_w;
@@ -182,40 +182,33 @@ __global__ __launch_bounds__(kWave, WS_X2Y_MINW) void fused_x2y_kernel(FusedArgs
             store_row(y0 - 1, Z);
             return;
         }
-        const V3<VT> k1 = stage_tend<POW2, XC, YC>(e, R - 1, g, yR2, yR1, yR0, a.sp1, a.gravity, a.coriolis_f);
+        const V3<VT> k1 = stage_tend<MODE, XC, YC>(e, R - 1, g, yR2, yR1, yR0, a.sp1, a.gravity, a.coriolis_f);
         if constexpr (NST == 1) {
-            store_row(R - 1, axpy(yR1, a.c_dt, k1));  // Euler: y + dt k
+            store_row(R - 1, axpy<MODE>(yR1, a.c_dt, k1));  // Euler: y + dt k
         } else {
-            const V3<VT> s1 = axpy(yR1, a.c_half, k1);  // y + (0.5f dt) k
+            const V3<VT> s1 = axpy<MODE>(yR1, a.c_half, k1);  // y + (0.5f dt) k
             if constexpr (on(2)) {
-                const V3<VT> k2 = stage_tend<POW2, XC, YC>(e, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
+                const V3<VT> k2 = stage_tend<MODE, XC, YC>(e, R - 2, g, S1[r2(-3)], S1[r2(-2)], s1, a.sp2,
                                                            a.gravity, a.coriolis_f);
                 if constexpr (NST == 2) {
-                    store_row(R - 2, axpy(yR2, a.c_dt, k2));  // RK2: y + dt k2
+                    store_row(R - 2, axpy<MODE>(yR2, a.c_dt, k2));  // RK2: y + dt k2
                 } else {
-                    const V3<VT> s2 = axpy(yR2, a.c_half, k2);
+                    const V3<VT> s2 = axpy<MODE>(yR2, a.c_half, k2);
                     if constexpr (on(3)) {
-                        const V3<VT> k3 = stage_tend<POW2, XC, YC>(e, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
+                        const V3<VT> k3 = stage_tend<MODE, XC, YC>(e, R - 3, g, S2[r2(-4)], S2[r2(-3)], s2, a.sp2,
                                                                    a.gravity, a.coriolis_f);
-                        const V3<VT> s3 = axpy(Y[r2(-3)], a.c_dt, k3);
+                        const V3<VT> s3 = axpy<MODE>(Y[r2(-3)], a.c_dt, k3);
                         if constexpr (on(4)) {
-                            const V3<VT> k4 = stage_tend<POW2, XC, YC>(e, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3,
+                            const V3<VT> k4 = stage_tend<MODE, XC, YC>(e, R - 4, g, S3[r2(-5)], S3[r2(-4)], s3,
                                                                        a.sp2, a.gravity, a.coriolis_f);
                             // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
-                            const T two = T(2);
-                            const V3<VT>& y4 = Y[r2(-4)];
-                            const V3<VT>& kk2 = K2[r2(-4)];
-                            const V3<VT>& kk3 = K3[r2(-4)];
-                            V3<VT> o;
-                            o.u = y4.u + a.c_dt6 * (((k4.u + two * kk2.u) + two * kk3.u) + k4.u);
-                            o.v = y4.v + a.c_dt6 * (((k4.v + two * kk2.v) + two * kk3.v) + k4.v);
-                            o.h = y4.h + a.c_dt6 * (((k4.h + two * kk2.h) + two * kk3.h) + k4.h);
+                            const V3<VT> o = rk4_final<MODE>(Y[r2(-4)], a.c_dt6, k4, K2[r2(-4)], K3[r2(-4)]);
                             store_row(R - 4, o);
                         } else {
                             store_row(y0 - 1, Z);
                         }
                         S3[r2(-3)] = s3;
-                        K3[r2(-3)] = k3;
+                        K3[r2(-3)] = rk4_keep3<MODE>(K2[r2(-3)], k3);
                     } else {
                         store_row(y0 - 1, Z);
                     }
@@ -276,19 +269,19 @@ hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom&
     const int64_t span = (int64_t)(a.seg_rows + 2 * nstages + 12 + 8) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nblocks), block(kWave);
-    const int sp_mode = fused_sp_mode(a);
 #define WS_X2Y_GO(N, M) hipLaunchKernelGGL((fused_x2y_kernel<T, N, M>), grid, block, 0, s, a, g, nstrips, nsegs)
-#define WS_X2Y_LAUNCH(N)                                 \
-    if (sp_mode == kSpScaled) WS_X2Y_GO(N, kSpScaled);   \
-    else if (sp_mode == kSpMul) WS_X2Y_GO(N, kSpMul);    \
-    else WS_X2Y_GO(N, kSpDiv);
+#define WS_X2Y_G1(M) WS_X2Y_GO(1, M)
+#define WS_X2Y_G2(M) WS_X2Y_GO(2, M)
+#define WS_X2Y_G4(M) WS_X2Y_GO(4, M)
     switch (nstages) {
-        case 1: WS_X2Y_LAUNCH(1) break;
-        case 2: WS_X2Y_LAUNCH(2) break;
-        case 4: WS_X2Y_LAUNCH(4) break;
+        case 1: WS_SP_DISPATCH(a.sp_mode, WS_X2Y_G1) break;
+        case 2: WS_SP_DISPATCH(a.sp_mode, WS_X2Y_G2) break;
+        case 4: WS_SP_DISPATCH(a.sp_mode, WS_X2Y_G4) break;
         default: return hipErrorInvalidValue;
     }
-#undef WS_X2Y_LAUNCH
+#undef WS_X2Y_G1
+#undef WS_X2Y_G2
+#undef WS_X2Y_G4
 #undef WS_X2Y_GO
     return hipGetLastError();
 }

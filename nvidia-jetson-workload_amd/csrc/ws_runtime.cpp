@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -21,6 +23,7 @@
 #include "ws_abi.h"
 #include "ws_comm.h"
 #include "ws_fused.h"
+#include "ws_halo.h"
 #include "ws_ic.h"
 #include "ws_internal.h"
 #include "ws_timer.h"
@@ -211,8 +214,7 @@ void convert(Dst* d, const Src* s, size_t n) {
 // ------------------------------------------------------------------------------------
 // simulation
 // ------------------------------------------------------------------------------------
-enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDpp = ws::kFusedDpp, kKernX2 = ws::kFusedX2,
-                         kKernDppDma = ws::kFusedDppDma, kKernDppLdsY = ws::kFusedDppLdsY, kKernX2Y = ws::kFusedX2Y };
+enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDppLdsY = ws::kFusedDppLdsY, kKernX2Y = ws::kFusedX2Y };
 
 struct ws_sim {
     ws_config_t cfg{};
@@ -242,17 +244,18 @@ struct ws_sim {
     bool own_stream = true;
     bool in_group = false;                              // a slab of a ws_group (local halo transport)
     bool fused = true;       // one fused kernel per step (WS_FUSED=0: one kernel per RK stage)
-    int kernel = kKernDpp;    // fused kernel variant (WS_KERNEL=x2|dpp|lds fixes it)
+    int kernel = kKernX2Y;    // fused kernel variant (WS_KERNEL=x2y|dppy|lds fixes it)
     int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
     bool align = false;       // strip output windows on whole 128-byte lines (WS_ALIGN fixes it)
     bool kernel_fixed = false, seg_fixed = false, align_fixed = false;
-    bool scaled = false;      // WS_SCALED=1: scaled tendencies (opt-in, ws_fused.h)
+    int numerics = WS_NUMERICS_EXACT;  // fused kernels: exact or fast numerics (ws_fused.h)
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
     int32_t want_blocks_override = 0;  // WS_WANT_BLOCKS
     // slab decomposition
     ws::SlabComm* comm = nullptr;
+    ws::HaloStaging* staging = nullptr;  // slab of a group: its halo messages (group_exchange)
     int32_t row0 = 0;
 
     int out_w(int nst) const { return ws::fused_out_w(kernel, nst, (int)elem_size(dtype), align); }
@@ -273,7 +276,7 @@ struct ws_sim {
     // warm-up rows stay a small overhead. The autotuner also tries other counts.
     int32_t seg_rows(int nst) const {
         if (seg_override > 0) return seg_override;
-        int64_t want_blocks = kernel == kKernX2 || kernel == kKernX2Y ? 2048 : (kernel == kKernDpp || kernel == kKernDppDma || kernel == kKernDppLdsY) ? 4096 : 512;
+        int64_t want_blocks = kernel == kKernX2Y ? 2048 : kernel == kKernDppLdsY ? 4096 : 512;
         if (want_blocks_override > 0) want_blocks = want_blocks_override;
         return seg_for_blocks(nst, want_blocks, 24 * nst);
     }
@@ -365,15 +368,14 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
-    // opt-in scaled tendencies (ws_fused.h): not bit-exact in the subnormal range
-    if (s->scaled) ws::scale_tendencies(a);
+    // numerics (ws_fused.h): exact = the reference's evaluation order, bit-identical;
+    // fast = re-associated with FMAs (isotropic spacing; otherwise exact)
+    if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
+    else a.sp_mode = ws::exact_sp_mode(a);
     const ws::Geom g = c->geom();
     switch (s->kernel) {
-        case kKernX2: WS_HIP_CHECK(ws::launch_fused_step_x2<T>(nst, a, g, st)); break;
         case kKernX2Y: WS_HIP_CHECK(ws::launch_fused_step_x2y<T>(nst, a, g, st)); break;
-        case kKernDpp: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppVgpr)); break;
-        case kKernDppDma: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppDma)); break;
-        case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dpp<T>(nst, a, g, st, ws::kDppLdsY)); break;
+        case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(nst, a, g, st)); break;
         default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st)); break;
     }
     ++s->last_launches;
@@ -480,9 +482,7 @@ int plan_steps(const ws_sim* s, int n) {
 // reads the current state and writes the next-state buffer, which the real step then
 // overwrites, so tuning leaves no trace in the results.
 template <typename T>
-void autotune(ws_sim* s) {
-    s->tuned = true;
-    if (!use_fused(s) || s->kernel_fixed) return;
+void autotune_time(ws_sim* s) {
     const int nst = fused_stages(s);
     struct Cand {
         int kernel, seg;
@@ -491,7 +491,7 @@ void autotune(ws_sim* s) {
     };
     std::vector<Cand> cands;
     const int fixed_seg = s->seg_override;
-    for (int k : {kKernDpp, kKernDppDma, kKernDppLdsY, kKernX2, kKernX2Y, kKernLds}) {
+    for (int k : {kKernDppLdsY, kKernX2Y, kKernLds}) {
         for (bool al : {false, true}) {
             if (s->align_fixed && al != s->align) continue;
             s->kernel = k;
@@ -562,6 +562,99 @@ void autotune(ws_sim* s) {
     s->seg_override = best->seg;
     s->align = best->align;
     s->last_launches = 0;
+}
+
+// Autotune results, per process (and optionally a file, WS_TUNE_CACHE=path): a drop-in user
+// creating many simulations of one shape pays the tuning once. The key is everything the
+// ranking depends on.
+struct TuneKey {
+    int32_t W, H, L, dtype, nst, numerics, top, bot, block, device;
+    bool operator<(const TuneKey& o) const {
+        return std::memcmp(this, &o, sizeof(TuneKey)) < 0;
+    }
+};
+struct TuneChoice {
+    int32_t kernel, seg, align;
+};
+std::mutex g_tune_mu;
+std::map<TuneKey, TuneChoice> g_tune_cache;
+bool g_tune_file_loaded = false;
+
+TuneKey tune_key(const ws_sim* s) {
+    const ws_grid* g = s->slot[0];
+    TuneKey k;
+    std::memset(&k, 0, sizeof(k));
+    k.W = g->W; k.H = g->H; k.L = g->L; k.dtype = s->dtype; k.nst = fused_stages(s);
+    k.numerics = s->numerics; k.top = g->top_clamp; k.bot = g->bot_clamp; k.block = s->block;
+    k.device = s->device;
+    return k;
+}
+
+void tune_file_load_locked() {
+    if (g_tune_file_loaded) return;
+    g_tune_file_loaded = true;
+    const char* path = std::getenv("WS_TUNE_CACHE");
+    if (!path) return;
+    FILE* f = std::fopen(path, "r");
+    if (!f) return;
+    TuneKey k;
+    TuneChoice c;
+    std::memset(&k, 0, sizeof(k));
+    while (std::fscanf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d", &k.W, &k.H, &k.L, &k.dtype, &k.nst, &k.numerics,
+                       &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg, &c.align) == 13)
+        if (c.kernel == kKernLds || c.kernel == kKernDppLdsY || c.kernel == kKernX2Y) g_tune_cache[k] = c;
+    std::fclose(f);
+}
+
+void tune_file_append_locked(const TuneKey& k, const TuneChoice& c) {
+    const char* path = std::getenv("WS_TUNE_CACHE");
+    if (!path) return;
+    if (FILE* f = std::fopen(path, "a")) {
+        std::fprintf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d\n", k.W, k.H, k.L, k.dtype, k.nst, k.numerics, k.top,
+                     k.bot, k.block, k.device, c.kernel, c.seg, c.align);
+        std::fclose(f);
+    }
+}
+
+// Pick the variant for this simulation: from the cache, or by timing (autotune_time). A slab
+// of a multi-rank decomposition takes rank 0's choice (one broadcast), so every rank runs the
+// same kernel and segment length and no rank runs behind on a different pick.
+template <typename T>
+void autotune(ws_sim* s) {
+    s->tuned = true;
+    if (!use_fused(s)) return;
+    const bool lead = !s->comm || s->comm->rank() == 0;
+    if (lead && !s->kernel_fixed) {
+        const TuneKey key = tune_key(s);
+        bool hit = false;
+        {
+            std::lock_guard<std::mutex> lk(g_tune_mu);
+            tune_file_load_locked();
+            auto it = g_tune_cache.find(key);
+            if (it != g_tune_cache.end() && !s->seg_fixed && !s->align_fixed) {
+                s->kernel = it->second.kernel;
+                s->seg_override = it->second.seg;
+                s->align = it->second.align != 0;
+                hit = true;
+            }
+        }
+        if (!hit) {
+            autotune_time<T>(s);
+            if (!s->seg_fixed && !s->align_fixed) {
+                std::lock_guard<std::mutex> lk(g_tune_mu);
+                const TuneChoice c{s->kernel, s->seg_override, s->align ? 1 : 0};
+                g_tune_cache[key] = c;
+                tune_file_append_locked(key, c);
+            }
+        }
+    }
+    if (s->comm && s->comm->nranks() > 1) {
+        int32_t v[3] = {s->kernel, s->seg_override, s->align ? 1 : 0};
+        s->comm->broadcast_i32(v, 3, 0, s->stream);
+        s->kernel = v[0];
+        s->seg_override = v[1];
+        s->align = v[2] != 0;
+    }
 }
 
 void run_steps(ws_sim* s, int k) {
@@ -637,6 +730,7 @@ void sim_free(ws_sim* s) {
     if (s->aux) (void)hipStreamDestroy(s->aux);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
     delete s->comm;
+    delete s->staging;
     delete s;
 }
 
@@ -676,14 +770,17 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         const int W = cfg->grid_width, H = local_rows, L = cfg->num_levels;
         for (int i = 0; i < 2; ++i) s->slot[i] = new_grid(W, H, L, s->dtype, s->device, 8, s->stream);
         if (const char* e = std::getenv("WS_FUSED")) s->fused = std::atoi(e) != 0;
-        s->scaled = env_int("WS_SCALED", 0) != 0;
+        // numerics: fast for fp64 (north_star tolerance), exact for fp32; WS_NUMERICS overrides
+        s->numerics = s->dtype == WS_F64 ? WS_NUMERICS_FAST : WS_NUMERICS_EXACT;
+        if (const char* e = std::getenv("WS_NUMERICS")) {
+            require(std::strcmp(e, "exact") == 0 || std::strcmp(e, "fast") == 0, WS_ERR_INVALID,
+                    "WS_NUMERICS must be exact or fast");
+            s->numerics = std::strcmp(e, "fast") == 0 ? WS_NUMERICS_FAST : WS_NUMERICS_EXACT;
+        }
         if (const char* e = std::getenv("WS_KERNEL")) {
-            s->kernel = std::strcmp(e, "lds") == 0      ? kKernLds
-                        : std::strcmp(e, "dpp") == 0    ? kKernDpp
-                        : std::strcmp(e, "dppdma") == 0 ? kKernDppDma
-                        : std::strcmp(e, "dppy") == 0   ? kKernDppLdsY
-                        : std::strcmp(e, "x2y") == 0    ? kKernX2Y
-                                                        : kKernX2;
+            require(std::strcmp(e, "lds") == 0 || std::strcmp(e, "dppy") == 0 || std::strcmp(e, "x2y") == 0,
+                    WS_ERR_INVALID, "WS_KERNEL must be x2y, dppy or lds");
+            s->kernel = std::strcmp(e, "lds") == 0 ? kKernLds : std::strcmp(e, "dppy") == 0 ? kKernDppLdsY : kKernX2Y;
             s->kernel_fixed = true;
         }
         if (const char* e = std::getenv("WS_WANT_BLOCKS")) s->want_blocks_override = std::atoi(e);
@@ -1330,6 +1427,53 @@ int ws_sim_fused_variant(const ws_sim_t* s, int32_t* kernel, int32_t* seg_rows, 
     });
 }
 
+int ws_sim_set_numerics(ws_sim_t* s, int32_t mode) {
+    return guarded([&] {
+        require(s != nullptr, WS_ERR_INVALID, "null sim");
+        require(mode == WS_NUMERICS_EXACT || mode == WS_NUMERICS_FAST, WS_ERR_INVALID,
+                "numerics must be WS_NUMERICS_EXACT or WS_NUMERICS_FAST");
+        if (mode != s->numerics && !s->kernel_fixed) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank
+        s->numerics = mode;
+    });
+}
+
+int ws_sim_get_numerics(const ws_sim_t* s, int32_t* mode) {
+    return guarded([&] {
+        require(s && mode, WS_ERR_INVALID, "null pointer");
+        *mode = s->numerics;
+    });
+}
+
+int ws_slab_exchange_plan(int32_t width, int32_t rows, int32_t levels, int32_t dtype, int32_t rank, int32_t nranks,
+                          int32_t nfields, int32_t depth, ws_xfer_t* out, int32_t capacity, int32_t* count,
+                          int64_t* pitch, int64_t* level_stride) {
+    return guarded([&] {
+        require(width > 0 && rows > 0 && levels > 0, WS_ERR_INVALID, "Grid dimensions must be positive");
+        require(dtype == WS_F32 || dtype == WS_F64, WS_ERR_INVALID, "bad dtype");
+        require(nranks >= 1 && rank >= 0 && rank < nranks, WS_ERR_INVALID, "bad rank / nranks");
+        require(nfields >= 1 && nfields <= ws::kMaxHaloFields, WS_ERR_INVALID, "bad field count");
+        require(depth >= 1 && depth <= ws::kHalo && depth <= rows, WS_ERR_INVALID, "bad halo depth");
+        // the slab grids' layout (grid_alloc)
+        ws::Geom g{};
+        g.W = width; g.H = rows; g.L = levels;
+        g.pitch = ((int64_t)width + 63) / 64 * 64;
+        g.lstride = ((int64_t)rows + 2 * ws::kHalo) * g.pitch;
+        g.top_clamp = rank == 0; g.bot_clamp = rank == nranks - 1; g.halo = ws::kHalo;
+        const auto x = ws::make_halo_plan(g, (int)elem_size(dtype), rank, nranks, nfields, depth).xfers();
+        if (count) *count = (int32_t)x.size();
+        if (pitch) *pitch = g.pitch;
+        if (level_stride) *level_stride = g.lstride;
+        if (out) {
+            require(capacity >= (int32_t)x.size(), WS_ERR_INVALID, "plan capacity too small");
+            for (size_t i = 0; i < x.size(); ++i) {
+                out[i].peer = x[i].peer; out[i].kind = x[i].kind; out[i].field = x[i].field;
+                out[i].level = x[i].level; out[i].offset = x[i].offset; out[i].bytes = x[i].bytes;
+                out[i].msg_offset = x[i].msg_offset;
+            }
+        }
+    });
+}
+
 int ws_sim_comm_barrier(ws_sim_t* s) {
     return guarded([&] {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
@@ -1355,36 +1499,43 @@ struct ws_group {
 
 namespace {
 
-// pull `depth` halo rows of u, v, h for slab r from its neighbours' current grids
-template <typename T>
-void group_exchange(ws_group* gr, int r, int depth) {
-    ws_sim* s = gr->slabs[r];
-    const ws_grid* me = s->slot[s->cur];
-    const size_t es = sizeof(T), row = (size_t)me->pitch * es, bytes = row * depth;
-    for (int f = 0; f < 3; ++f) {
-        for (int l = 0; l < me->L; ++l) {
-            char* mine = (char*)me->f[f] + (size_t)l * me->lstride * es;
-            if (r > 0) {
-                const ws_grid* up = gr->slabs[r - 1]->slot[gr->slabs[r - 1]->cur];
-                const char* src = (const char*)up->f[f] + (size_t)l * up->lstride * es + (size_t)(up->H - depth) * row;
-                WS_HIP_CHECK(hipMemcpyAsync(mine - bytes, src, bytes, hipMemcpyDeviceToDevice, gr->stream));
-            }
-            if (r + 1 < (int)gr->slabs.size()) {
-                const ws_grid* dn = gr->slabs[r + 1]->slot[gr->slabs[r + 1]->cur];
-                const char* src = (const char*)dn->f[f] + (size_t)l * dn->lstride * es;
-                WS_HIP_CHECK(hipMemcpyAsync(mine + (size_t)me->H * row, src, bytes, hipMemcpyDeviceToDevice,
-                                            gr->stream));
-            }
-        }
+// The halo exchange of every slab of the group, by the plan of ws_halo.h: each slab packs
+// its neighbour messages (halo_pack), the messages move by device copies into the
+// neighbours' receive staging (what RCCL does between processes, ws_comm.cpp), and each slab
+// unpacks them -- the same plan and kernels as the multi-process path.
+void group_exchange(ws_group* gr, int nfields, int depth) {
+    const int n = (int)gr->slabs.size();
+    std::vector<ws::HaloPlan> plans(n);
+    std::vector<ws::HaloFields> hf(n);
+    for (int r = 0; r < n; ++r) {
+        ws_sim* s = gr->slabs[r];
+        const ws_grid* me = s->slot[s->cur];
+        plans[r] = ws::make_halo_plan(me->geom(), (int)elem_size(me->dtype), r, n, nfields, depth);
+        if (!s->staging) s->staging = new ws::HaloStaging;
+        s->staging->ensure(plans[r].msg_bytes());
+        for (int f = 0; f < nfields; ++f) hf[r].f[f] = (char*)me->f[f];
+        for (int side = 0; side < 2; ++side)
+            if (plans[r].has[side])
+                WS_HIP_CHECK(ws::halo_pack(plans[r], hf[r], side, s->staging->send[side], gr->stream));
     }
+    for (int r = 0; r < n; ++r)
+        for (int side = 0; side < 2; ++side) {
+            if (!plans[r].has[side]) continue;
+            ws_sim* peer = gr->slabs[plans[r].peer[side]];
+            WS_HIP_CHECK(hipMemcpyAsync(peer->staging->recv[1 - side], gr->slabs[r]->staging->send[side],
+                                        (size_t)plans[r].msg_bytes(), hipMemcpyDeviceToDevice, gr->stream));
+        }
+    for (int r = 0; r < n; ++r)
+        for (int side = 0; side < 2; ++side)
+            if (plans[r].has[side])
+                WS_HIP_CHECK(ws::halo_unpack(plans[r], hf[r], side, gr->slabs[r]->staging->recv[side], gr->stream));
 }
 
 template <typename T>
 void group_step(ws_group* gr) {
     ws_sim* s0 = gr->slabs[0];
     if (s0->block_pos == 0) {  // a block starts: the block's halo, by device copies
-        const int depth = s0->block * fused_stages(s0);
-        for (int r = 0; r < (int)gr->slabs.size(); ++r) group_exchange<T>(gr, r, depth);
+        group_exchange(gr, 3, s0->block * fused_stages(s0));
     }
     for (ws_sim* s : gr->slabs) step_begin<T>(s);
     for (ws_sim* s : gr->slabs) step_end<T>(s);
@@ -1472,9 +1623,7 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
         }
         WS_HIP_CHECK(hipEventRecord(s0->ev1, gr->stream));
         if (k > 0) {  // seam diagnostics need the neighbours' current rows (see run_steps)
-            for (int r = 0; r < (int)gr->slabs.size(); ++r)
-                if (s0->dtype == WS_F64) group_exchange<double>(gr, r, 1);
-                else group_exchange<float>(gr, r, 1);
+            group_exchange(gr, 2, 1);
             for (ws_sim* s : gr->slabs) materialize_diag(s->slot[s->cur]);
         }
         WS_HIP_CHECK(hipStreamSynchronize(gr->stream));

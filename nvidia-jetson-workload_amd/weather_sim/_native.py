@@ -20,6 +20,7 @@ WS_OK, WS_ERR_INVALID, WS_ERR_DEVICE, WS_ERR_SHAPE, WS_ERR_UNSUPPORTED, WS_ERR_C
 WS_F32, WS_F64 = 0, 1
 FIELD = {"u": 0, "v": 1, "h": 2, "p": 3, "t": 4, "q": 5, "vorticity": 6, "divergence": 7}
 COMM_ID_BYTES = 128
+NUMERICS = {"exact": 0, "fast": 1}
 
 
 class ws_config_t(ctypes.Structure):
@@ -33,6 +34,12 @@ class ws_config_t(ctypes.Structure):
         ("max_time", ctypes.c_double), ("max_steps", ctypes.c_int32), ("output_interval", ctypes.c_int32),
         ("random_seed", ctypes.c_uint32),
     ]
+
+
+class ws_xfer_t(ctypes.Structure):
+    _fields_ = [("peer", ctypes.c_int32), ("kind", ctypes.c_int32), ("field", ctypes.c_int32),
+                ("level", ctypes.c_int32), ("offset", ctypes.c_int64), ("bytes", ctypes.c_int64),
+                ("msg_offset", ctypes.c_int64)]
 
 
 class ws_metrics_t(ctypes.Structure):
@@ -116,6 +123,9 @@ SIGNATURES = {
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
     "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
+    "ws_sim_set_numerics": [_P, _I],
+    "ws_sim_get_numerics": [_P, _PI],
+    "ws_slab_exchange_plan": [_I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ws_xfer_t), _I, _PI, _PL, _PL],
     "ws_bvort_create": [ctypes.POINTER(ws_config_t), _PP],
     "ws_bvort_destroy": [_P],
     "ws_bvort_set_vorticity": [_P, _P, _I, _I, _I],
@@ -177,3 +187,16 @@ def is_available():
     a = ctypes.c_int32(0)
     check(lib.ws_is_available(ctypes.byref(a)))
     return bool(a.value)
+
+
+def exchange_plan(width, rows, levels, fp64, rank, nranks, nfields, depth):
+    """The library's halo exchange plan (ws_slab_exchange_plan): (list of ws_xfer_t,
+    pitch, level_stride) for one slab of the decomposition."""
+    n, pitch, lstride = ctypes.c_int32(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    dt = WS_F64 if fp64 else WS_F32
+    check(lib.ws_slab_exchange_plan(width, rows, levels, dt, rank, nranks, nfields, depth, None, 0,
+                                    ctypes.byref(n), ctypes.byref(pitch), ctypes.byref(lstride)))
+    buf = (ws_xfer_t * max(1, n.value))()
+    check(lib.ws_slab_exchange_plan(width, rows, levels, dt, rank, nranks, nfields, depth, buf, n.value,
+                                    ctypes.byref(n), None, None))
+    return list(buf[:n.value]), pitch.value, lstride.value

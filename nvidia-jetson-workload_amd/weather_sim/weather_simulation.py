@@ -675,9 +675,18 @@ class WeatherSimulation:
         in use (chosen at the first run)."""
         k, seg, cols = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg), ctypes.byref(cols)))
-        return ({-1: "stage_kernels", 0: "fused_lds", 1: "fused_dpp", 2: "fused_x2", 3: "fused_dppdma",
-                 4: "fused_dppy", 5: "fused_x2y"}[k.value], seg.value,
+        return ({-1: "stage_kernels", 0: "fused_lds", 4: "fused_dppy", 5: "fused_x2y"}[k.value], seg.value,
                 cols.value)
+
+    def set_numerics(self, mode):
+        """Extension: "exact" (bit-for-bit with the reference) or "fast" (FMA re-association,
+        the fp64 default; ws_hip.h WS_NUMERICS_*) for the fused step kernels."""
+        check(lib.ws_sim_set_numerics(self._h, _native.NUMERICS[mode]))
+
+    def get_numerics(self):
+        m = ctypes.c_int32()
+        check(lib.ws_sim_get_numerics(self._h, ctypes.byref(m)))
+        return {v: k for k, v in _native.NUMERICS.items()}[m.value]
 
     def comm_allreduce_max(self, value):
         out = ctypes.c_double()

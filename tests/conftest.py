@@ -14,6 +14,14 @@ for p in (ROOT, PKG_DIR):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+@pytest.fixture(autouse=True)
+def _exact_numerics(monkeypatch):
+    """Every test runs the fused kernels in exact numerics (bit-for-bit with the reference)
+    unless it asks otherwise: fp64 simulations default to fast numerics (ws_hip.h), which
+    tests/test_gpu_numerics.py covers against its tolerance."""
+    monkeypatch.setenv("WS_NUMERICS", "exact")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running full-size case")

@@ -52,7 +52,7 @@ def test_one_rank_rccl_slab_matches_single_domain(method, fp64):
 
 
 @pytest.mark.parametrize("block", ["1", "2", "3"])
-@pytest.mark.parametrize("kernel", ["dpp", "dppdma", "dppy", "x2", "x2y", "lds"])
+@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 def test_slab_blocks_are_bitwise(block, kernel, method, monkeypatch):
     """Slabs advance `block` steps per halo exchange (block x NST halo rows, steps computed

@@ -1,6 +1,6 @@
-"""Column-pair ("x2") fused kernel edge cases, bitwise vs the CPU oracle: odd widths (the
-last pair straddles x = W-1), widths narrower than one 128-column strip, widths that end
-exactly on a strip boundary, and non-power-of-two spacing (IEEE-divide instantiation)."""
+"""Fused-kernel strip edge cases, bitwise vs the CPU oracle: odd widths (x2y's last column
+pair straddles x = W-1), widths narrower than one strip, widths that end exactly on a strip
+boundary, non-power-of-two spacing (IEEE-divide instantiation), line-aligned strips."""
 import numpy as np
 import pytest
 
@@ -36,23 +36,25 @@ def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3):
         np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=f"W={W} {k}")
 
 
-@pytest.mark.parametrize("W", [2, 3, 7, 64, 120, 121, 127, 128, 129, 240, 241, 333])
+@pytest.mark.parametrize("W", [2, 3, 7, 56, 57, 64, 120, 121, 127, 128, 129, 240, 241, 333])
+@pytest.mark.parametrize("kernel", ["dppy", "x2y"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_x2_widths(W, method, fp64, monkeypatch):
-    monkeypatch.setenv("WS_KERNEL", "x2")
+def test_strip_widths(W, kernel, method, fp64, monkeypatch):
+    monkeypatch.setenv("WS_KERNEL", kernel)
     monkeypatch.setenv("WS_SEG_ROWS", "7")
     run_both(W, 29, method, fp64, 5)
 
 
+@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
-def test_x2_non_pow2(method, monkeypatch):
-    monkeypatch.setenv("WS_KERNEL", "x2")
+def test_non_pow2_spacing(kernel, method, monkeypatch):
+    monkeypatch.setenv("WS_KERNEL", kernel)
     run_both(301, 40, method, True, 4, dx=0.75, dy=1.3)
 
 
 @pytest.mark.parametrize("W", [61, 300, 700])
-@pytest.mark.parametrize("kernel", ["dpp", "dppdma", "dppy", "x2", "x2y", "lds"])
+@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_line_aligned_strips(W, kernel, method, fp64, monkeypatch):
