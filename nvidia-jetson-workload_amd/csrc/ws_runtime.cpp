@@ -127,9 +127,14 @@ int64_t env_int(const char* name, int64_t dflt) {
     return e ? std::atoll(e) : dflt;
 }
 
+// row pitch (elements) and level stride of a W x H grid: rows padded to 64 elements, kHalo
+// halo rows above and below every level (the layout ws_slab_exchange_plan reports)
+int64_t layout_pitch(int64_t W) { return (W + 63) / 64 * 64 + env_int("WS_PITCH_PAD", 0) / 64 * 64; }
+int64_t layout_lstride(int64_t H, int64_t pitch) { return (H + 2 * ws::kHalo) * pitch; }
+
 void grid_alloc(ws_grid* g, unsigned nfields) {
-    g->pitch = ((int64_t)g->W + 63) / 64 * 64 + env_int("WS_PITCH_PAD", 0) / 64 * 64;
-    g->lstride = ((int64_t)g->H + 2 * ws::kHalo) * g->pitch;
+    g->pitch = layout_pitch(g->W);
+    g->lstride = layout_lstride(g->H, g->pitch);
     g->nfields = nfields;
     const size_t es = elem_size(g->dtype);
     const size_t stagger = (size_t)env_int("WS_FIELD_STAGGER", 0) / 256 * 256;  // bytes, field i offset by i*stagger
@@ -1456,8 +1461,8 @@ int ws_slab_exchange_plan(int32_t width, int32_t rows, int32_t levels, int32_t d
         // the slab grids' layout (grid_alloc)
         ws::Geom g{};
         g.W = width; g.H = rows; g.L = levels;
-        g.pitch = ((int64_t)width + 63) / 64 * 64;
-        g.lstride = ((int64_t)rows + 2 * ws::kHalo) * g.pitch;
+        g.pitch = layout_pitch(width);
+        g.lstride = layout_lstride(rows, g.pitch);
         g.top_clamp = rank == 0; g.bot_clamp = rank == nranks - 1; g.halo = ws::kHalo;
         const auto x = ws::make_halo_plan(g, (int)elem_size(dtype), rank, nranks, nfields, depth).xfers();
         if (count) *count = (int32_t)x.size();
