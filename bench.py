@@ -96,17 +96,27 @@ def max_over_ranks(dist, seconds):
     return float(t[0])
 
 
-def stagewise_words(model, method):
-    """SURVEY §8(d) words per cell-update of a stage-by-stage step (non-SWE RK4 runs RK2,
-    AB / semi-implicit run Euler: weather_simulation.cpp:117-158, 334-338)."""
-    if method == 2 and model != 0:
-        method = 1
-    return {0: 6, 1: 15, 2: 45}.get(method, 6)
+def host_cores():
+    """Cores this process may run on: its CPU affinity set, capped by a cgroup CPU quota
+    (cpu.max) when one is set -- on the GPU pool the affinity shows the whole machine while
+    the quota gives the box's share. Returns (cores, how it was determined)."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            if q < aff:
+                return q, f"cgroup cpu.max quota {quota}/{period} (affinity {aff} CPUs)"
+    except (OSError, ValueError):
+        pass
+    return aff, f"sched_getaffinity: {aff} CPUs"
 
 
 def cpu_baseline(conf, method, budget_s=20.0):
-    """Time the reference CPU solver (or the oracle port) on a bounded sample."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    """Time the reference CPU solver (or the oracle port) on a bounded sample, with one
+    OpenMP thread per host core this process may use (host_cores)."""
+    threads, how = host_cores()
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     variant = "f64" if conf["fp64"] else "f32"
     ref = os.path.join(ROOT, "oracle", "_ref", f"ws_ref_{variant}")
@@ -149,7 +159,7 @@ def cpu_baseline(conf, method, budget_s=20.0):
         what = "C oracle port (oracle/ws_oracle.c, -O3 -fopenmp)"
     return {"value": W * H * steps / secs, "unit": "cell-updates/s", "cores": threads, "kind": kind,
             "sample": f"{what}: {W}x{H}, {steps} steps after 1 warm-up step, {secs:.2f} s wall, "
-                      f"OMP_NUM_THREADS={threads}"}
+                      f"OMP_NUM_THREADS={threads} ({how})"}
 
 
 def bvort_words_per_cell(method, W, H):
@@ -396,13 +406,17 @@ def main():
 
     cells = conf["W"] * conf["H"] * conf["L"]
     value = cells * args.steps / elapsed
+    # CFL of the final state by the device max-reduction (outside the timed region; a
+    # collective over the ranks of a slab decomposition, so every rank calls it)
+    cfl, cfl_ms = sim.get_cfl(with_time=True)
     stats = sim.kernel_timing()
     variant, seg_rows, out_cols = sim.fused_variant()
+    tb = sim.steps_per_launch()
     dev_ms, launches = sim.last_run_stats()
     # dominant kernel = largest total device time
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
     achieved = bpl / (tot_ms / n * 1e-3) / 1e9
-    step_bytes = sum(b for (_, _, b) in stats.values())
+    step_bytes = sum(b for (_, _, b) in stats.values()) / tb  # one launch per kind covers tb steps
     traffic = None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
     if os.path.exists(tfile):
@@ -427,13 +441,22 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
-                     "seg_rows": seg_rows, "strip_out_cols": out_cols, "bytes_per_launch": bpl,
-                     "mean_launch_ms": tot_ms / n},
+                     "seg_rows": seg_rows, "strip_out_cols": out_cols, "steps_per_launch": tb,
+                     "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n,
+                     "byte_model": (f"algorithmic bytes per launch = 6 words per cell-update (read u, v, h + write "
+                                    f"u, v, h: the compulsory traffic of one time step) x {cells} cells x the {tb} "
+                                    f"step(s) one launch advances ({'f64' if conf['fp64'] else 'f32'}); traffic = "
+                                    f"rocprofv3 PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
+                                    f"profiles/traffic_{args.config}_{args.method}.json). A two-step launch reads y_n "
+                                    f"and writes y_(n+2) once, so its traffic is about half its algorithmic bytes: "
+                                    f"dram_gbs is the measured DRAM rate"
+                                    if variant != "stage_kernels" else "SURVEY 8(d) stage-kernel words per launch"),
+                     "dram_gbs": traffic / (tot_ms / n * 1e-3) / 1e9 if traffic else None},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
-        # SURVEY §8(d) prices the path as stage-by-stage passes (Euler 6w, RK2 15w, RK4 45w per
-        # cell): the rate that traffic would need at the measured launch time
-        "equivalent_stagewise_gbs": (stagewise_words(conf["model"], method) * (8 if conf["fp64"] else 4) * cells
-                                     / (tot_ms / n * 1e-3) / 1e9) if variant != "stage_kernels" else None,
+        "cfl": {"value": cfl, "reduction_ms": cfl_ms,
+                "gbs": 3 * (8 if conf["fp64"] else 4) * cells / world / (cfl_ms * 1e-3) / 1e9 if cfl_ms > 0 else None,
+                "note": "max((|u|+sqrt(gh))dt/dx, (|v|+sqrt(gh))dt/dy) of the final state; device DPP max-reduction "
+                        "reading u, v, h once (gbs = 3 words per local cell / reduction time)"},
         "kernel_stats": {f"stage{k}": {"launches": v[0], "mean_ms": v[1] / v[0], "bytes": v[2],
                                        "gbs": v[2] / (v[1] / v[0] * 1e-3) / 1e9} for k, v in stats.items()},
     }

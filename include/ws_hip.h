@@ -323,6 +323,22 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
  * position), and a slab decomposition uses rank 0's choice on every rank. */
 int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols);
 
+/* Time steps per fused launch the simulation's run() uses where it can (new; temporal
+ * blocking): 1, or 2 = the dppy kernel advances two steps per launch (y_n read once,
+ * y_{n+2} written once). Chosen by the autotuner (WS_TB=1|2 fixes it). A two-step launch
+ * runs only inside run(k >= 2), inside a slab block with room for both steps, and with the
+ * configured spacing on both grids; results are identical to two one-step launches. */
+int ws_sim_steps_per_launch(const ws_sim_t* sim, int32_t* steps);
+
+/* CFL number of the current state (new: the reference's dt is fixed and it has no CFL):
+ * max over cells of max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy), computed in
+ * the simulation's precision by a device max-reduction (one pass over u, v, h; DPP wave
+ * reductions); NaN if any cell is NaN or h < 0. *cfl = the maximum over all levels (and, on a
+ * slab of a multi-GPU decomposition, over all ranks: an RCCL max-allreduce, so every rank
+ * must call it); per_level (optional, nlevels >= num_levels entries) = per level; ms
+ * (optional) = device time of the reduction kernels. */
+int ws_sim_cfl(ws_sim_t* sim, double* cfl, double* per_level, int32_t nlevels, double* ms);
+
 /* ---- numerics mode of the fused step kernels ------------------------------------------
  * WS_NUMERICS_EXACT: the reference's arithmetic in the reference's evaluation order, no
  *   contraction: bit-for-bit equal to the CPU solver (weather_simulation.cpp:160-540).

@@ -85,6 +85,11 @@ double SlabComm::allreduce_max(double v, hipStream_t stream) {
     return out;
 }
 
+void SlabComm::allreduce_max_u64_device(uint64_t* d, int n, hipStream_t stream) {
+    if (nranks_ == 1 || n <= 0) return;
+    check(ncclAllReduce(d, d, (size_t)n, ncclUint64, ncclMax, (ncclComm_t)comm_, stream), "ncclAllReduce");
+}
+
 void SlabComm::barrier(hipStream_t stream) { (void)allreduce_max(0.0, stream); }
 
 }  // namespace ws

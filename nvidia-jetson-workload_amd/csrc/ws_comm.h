@@ -42,6 +42,9 @@ public:
     void broadcast_i32(int32_t* v, int n, int root, hipStream_t stream);
     // In-place max over ranks of one double (device scratch owned by the comm).
     double allreduce_max(double v, hipStream_t stream);
+    // In-place max over ranks of n uint64 values in DEVICE memory, enqueued on `stream` (the
+    // CFL reduction's per-level bit patterns, ws_reduce.hip)
+    void allreduce_max_u64_device(uint64_t* d, int n, hipStream_t stream);
     void barrier(hipStream_t stream);
 
 private:

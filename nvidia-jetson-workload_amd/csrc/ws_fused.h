@@ -86,8 +86,12 @@ hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, 
 // "dppy": independent 64-lane waves, one column per lane, horizontal neighbours by DPP lane
 // shifts, y rows staged by LDS-DMA and read from LDS in place.
 constexpr int kDppCols = 64;
+// nsteps = time steps per launch (1, or 2: temporal blocking, see ws_fused_dppy.hip)
 template <typename T>
-hipError_t launch_fused_step_dppy(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+hipError_t launch_fused_step_dppy(int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
+// one translation unit per (T, steps per launch): the kernel instantiations
+template <typename T, int NSTEP>
+hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs);
 // "x2y": as dppy with an adjacent column pair per lane (128-column strips).
 template <typename T>
 hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);

@@ -1,0 +1,324 @@
+// Fused multi-stage time step, wave-independent variant ("dppy"): one 64-lane wave per
+// column strip, horizontal neighbours by DPP lane shifts (wave_shr:1 / wave_shl:1) -- no
+// workgroup barrier -- and the y rows staged by LDS-DMA and read from LDS in place.
+//
+// Same march as ws_fused.hip (one kernel per time step; y read once, y' written once;
+// stage s = 1..NST computes row R - s while row R arrives; register rings indexed by a
+// compile-time phase), but every wave runs free: nothing synchronises it with any other
+// wave, so a wave waiting on HBM never holds its neighbours back. The price is halo
+// redundancy: a 64-column strip outputs 64 - 2*margin columns.
+//
+// y rows: LDS-DMA (buffer_load_dwordx4 ... lds, 16 bytes per lane: one instruction per
+// field moves kG = 16 / sizeof(T) rows of the strip) into a ring one group ahead; each body
+// reads the three rows stage 1 needs (R-2, R-1, R) straight from the ring, only rows R-3
+// and R-4 (the late stage updates) live in VGPRs -- three waves per SIMD fit (RK4 fp64).
+// The compiler does not order LDS reads after LDS-DMA writes, so the kernel waits itself:
+// every body issues exactly 3 stores and every kG-th body 3 DMAs, a fixed count of younger
+// vector-memory ops at each wait (kWaitN).
+//
+// Temporal blocking (NSTEP = 2): one launch advances two time steps. The march chains the
+// second step's stages behind the first's: the first step's output row (R - NST) is the
+// second step's "arriving" row, its last two rows sit in a register ring, and only the
+// second step's output is stored -- y_n is read once and y_{n+2} written once, halving the
+// HBM bytes per step, for a dependency cone twice as deep (margins of 2 NST columns, 4 NST
+// warm-up rows per segment).
+//
+// Arithmetic per cell: the reference's, in the reference's order
+// (weather_simulation.cpp:160-455, 473-540), or fast numerics (ws_fused.h) by spacing mode.
+#pragma once
+
+#include <type_traits>
+#include <utility>
+
+#include "ws_fused_dev.h"
+
+namespace ws {
+namespace {  // kernels: internal to each translation unit
+
+using namespace dev;
+
+constexpr int kWave = 64;
+
+// One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
+// XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
+// the neighbour index to the cell itself (weather_simulation.cpp:510-513).
+template <int MODE, bool XCLAMP, bool YCLAMP, typename T>
+__device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
+                                            const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav,
+                                            T cor) {
+    V3<T> l{from_left(mid.u), from_left(mid.v), from_left(mid.h)};
+    V3<T> r{from_right(mid.u), from_right(mid.v), from_right(mid.h)};
+    if constexpr (XCLAMP) {
+        l = V3<T>{xlo ? mid.u : l.u, xlo ? mid.v : l.v, xlo ? mid.h : l.h};
+        r = V3<T>{xhi ? mid.u : r.u, xhi ? mid.v : r.v, xhi ? mid.h : r.h};
+    }
+    if constexpr (YCLAMP) {
+        const bool ytop = (j == 0) && g.top_clamp;
+        const bool ybot = (j == g.H - 1) && g.bot_clamp;
+        const V3<T> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
+        const V3<T> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
+        return tend<MODE>(mid, l, r, t, b, sp, grav, cor);
+    } else {
+        return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
+    }
+}
+
+// s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
+// lgkmcnt[11:8], vmcnt[15:14]); the other counters at their maxima = not waited on
+constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// Per time step of a launch: the march's register rings (parity-indexed by row)
+template <typename T>
+struct StepRings {
+    V3<T> Y[2];                  // Y[r % 2] = the step's input row r, r <= R-3
+    V3<T> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
+    V3<T> K2[2], K3[2];          // RK4 stage-2 tendency / stage-3 keep (rk4_keep3) at row r
+    V3<T> O[2];                  // the step's last output rows (the next step's input), NSTEP > 1
+};
+
+template <typename T, int NST, int NSTEP, int MODE>
+__global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+    constexpr int kG = 16 / (int)sizeof(T);                // rows per DMA instruction
+    constexpr int kD = kG;                                  // DMA rows in flight (one group ahead)
+    constexpr int kNR = (kD + kG + 2 + kG - 1) / kG * kG;   // ring: rows R-2 .. R+kD+kG-1, whole groups
+    constexpr int kU = kNR;                                 // march unroll: ring slot == phase
+    constexpr int kNS = NST * NSTEP;                        // stages per launch (the cone depth)
+    // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on
+    constexpr int kNW = (2 * kNS + kU - 1) / kU < 3 ? (2 * kNS + kU - 1) / kU : 3;
+    // a group's DMA may overwrite only slots whose rows were read in an earlier body
+    static_assert(kU % kG == 0 && kU % 2 == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
+    static_assert(NSTEP == 1 || NSTEP == 2, "one or two steps per launch");
+    // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory LOADS
+    // issued after them (the DMAs in between, incl. the reading body's own). Stores are not
+    // counted: a store may complete before an older load, so a count that includes them can
+    // drop below the threshold while the group is still in flight (seen as stale rows at
+    // 4096^2). Loads complete in order.
+    constexpr int kWaitN = 3 * (kD / kG);
+
+    const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
+    const int strip = w % nstrips;
+    int y0, y1;
+    fused_rows(a, (w / nstrips) % nsegs, y0, y1);
+    const int level = w / (nstrips * nsegs);
+
+    const int lane = (int)threadIdx.x;
+    // left margin: the cone (kNS) rounded up to whole 16-byte chunks, so a strip's DMA chunks
+    // never straddle column 0 (a partly negative chunk is dropped whole by the range check)
+    constexpr int kM = (kNS + kG - 1) / kG * kG;
+    const int out_w = a.out_w;
+    const int x = strip * out_w - kM + lane;  // this lane's global column
+    const bool xout = x >= 0 && x < g.W && lane >= kM && lane < kM + out_w;
+    const bool xlo = x == 0, xhi = x == g.W - 1;
+
+    const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
+    const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
+
+    // Buffer addressing: one descriptor per field, based at this wave's first row (all
+    // wave-uniform, SGPRs), the row as a scalar byte offset, the lane's column as a fixed
+    // 32-bit voffset -- no per-row VALU address arithmetic. Stores of lanes outside the
+    // strip's output columns get an out-of-range voffset: the buffer range check drops them
+    // (no exec-mask branch). launch_fused_step_dppy checks the byte ranges fit.
+    const int64_t lofs = (int64_t)level * g.lstride;
+    const int rbase = max(y0 - kNS, row_lo);
+    const int rtop = min(row_hi, y1 + kNS + kU + kD + kG);  // past the last row the march fetches
+    const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
+    const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
+    const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
+    const auto ru = make_rsrc(a.in_u + ib, in_bytes), rv = make_rsrc(a.in_v + ib, in_bytes),
+               rh = make_rsrc(a.in_h + ib, in_bytes);
+    const auto wu = make_rsrc(a.out_u + ob, out_bytes), wv = make_rsrc(a.out_v + ob, out_bytes),
+               wh = make_rsrc(a.out_h + ob, out_bytes);
+    const uint32_t row_bytes = (uint32_t)g.pitch * sizeof(T);
+    const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : kDropped;
+
+    // Stores are issued for every row, unconditionally: rows outside [y0, y1) are dropped by
+    // the range check through the voffset (a branch around them makes the compiler's vmcnt
+    // bookkeeping merge both paths and drain the prefetch at every row).
+    auto store_row = [&](int j, const V3<T>& o) {
+        const bool row_ok = j >= y0 && j < y1;
+        const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
+        const uint32_t vo = row_ok ? soff : kDropped;
+        buf_store_nt<T>(o.u, wu, vo, so);
+        buf_store_nt<T>(o.v, wv, vo, so);
+        buf_store_nt<T>(o.h, wh, vo, so);
+    };
+
+    // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG
+    // consecutive slots (64 lanes x 16 B = kG rows of 64 columns)
+    __shared__ __attribute__((aligned(16))) T ring[3][kNR][kWave];
+    const int dk = lane / (kWave / kG);  // row of the group this lane fetches
+    const int dcol = (strip * out_w - kM) * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // 16-B aligned
+    auto dma = [&](int q, int slot) {  // rows q .. q + kG - 1 into slots slot .. slot + kG - 1
+        const int r = min(max(q + dk, row_lo), row_hi - 1);
+        // chunks left of column 0 (whole chunks: kM is chunk-aligned) wrap to huge offsets or
+        // read the previous row, chunks past the row end read the next row: margin lanes
+        // only, never read by an output lane
+        const uint32_t vo = (uint32_t)((r - rbase) * (int)row_bytes + dcol);
+        lds_dma16(ru, &ring[0][slot][0], vo);
+        lds_dma16(rv, &ring[1][slot][0], vo);
+        lds_dma16(rh, &ring[2][slot][0], vo);
+    };
+    auto read_row = [&](int slot) -> V3<T> { return V3<T>{ring[0][slot][lane], ring[1][slot][lane], ring[2][slot][lane]}; };
+
+    const V3<T> Z{T(0), T(0), T(0)};
+    StepRings<T> st[NSTEP];
+#pragma unroll
+    for (int q = 0; q < NSTEP; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) st[q].Y[i] = st[q].S1[i] = st[q].S2[i] = st[q].S3[i] = st[q].K2[i] = st[q].K3[i] = st[q].O[i] = Z;
+
+    const int R0 = y0 - kNS;
+    const int R1 = R0 + (y1 + kNS - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
+
+    // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
+    // stage s computes row Rq - s; the step's output row Rq - NST goes to `out`. Stage s of
+    // step q is stage gs = q NST + s of the launch's cone; `ON(gs)` says whether this body
+    // needs it (warm-up: the first bodies of a segment skip stages outside the segment's
+    // cone; whatever a body computes beyond the cone only ever reaches rows that are not
+    // stored). Ring slots are indexed by the parity of the body phase P.
+    auto step = [&](auto Qc, auto Pc, auto Xc, auto Yc, auto ONc, StepRings<T>& S, const V3<T>& i0,
+                    const V3<T>& i1, const V3<T>& i2, int Rq, V3<T>& out) {
+        constexpr int q = decltype(Qc)::value;
+        constexpr int P = decltype(Pc)::value;
+        constexpr bool XC = decltype(Xc)::value;
+        constexpr bool YC = decltype(Yc)::value;
+        constexpr auto on = [](int s) { return decltype(ONc){}(q * NST + s); };
+        constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
+        if constexpr (on(1)) {
+            // stage 1 of the launch reads the current grid (its spacing sp1); every later stage
+            // a temp / next grid (the config's spacing sp2; the host launches two steps at once
+            // only when sp1 == sp2)
+            const Spacing<T>& sp_in = q == 0 ? a.sp1 : a.sp2;
+            const V3<T> k1 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 1, g, i2, i1, i0, sp_in, a.gravity, a.coriolis_f);
+            if constexpr (NST == 1) {
+                out = axpy<MODE>(i1, a.c_dt, k1);  // Euler: y + dt k
+            } else {
+                const V3<T> s1 = axpy<MODE>(i1, a.c_half, k1);  // y + (0.5f dt) k
+                if constexpr (on(2)) {
+                    const V3<T> k2 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
+                                                              a.sp2, a.gravity, a.coriolis_f);
+                    if constexpr (NST == 2) {
+                        out = axpy<MODE>(i2, a.c_dt, k2);  // RK2: y + dt k2
+                    } else {
+                        const V3<T> s2 = axpy<MODE>(i2, a.c_half, k2);
+                        if constexpr (on(3)) {
+                            const V3<T> k3 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 3, g, S.S2[r2(-4)], S.S2[r2(-3)],
+                                                                      s2, a.sp2, a.gravity, a.coriolis_f);
+                            const V3<T> s3 = axpy<MODE>(S.Y[r2(-3)], a.c_dt, k3);
+                            if constexpr (on(4)) {
+                                const V3<T> k4 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 4, g, S.S3[r2(-5)],
+                                                                          S.S3[r2(-4)], s3, a.sp2, a.gravity,
+                                                                          a.coriolis_f);
+                                // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
+                                out = rk4_final<MODE>(S.Y[r2(-4)], a.c_dt6, k4, S.K2[r2(-4)], S.K3[r2(-4)]);
+                            }
+                            S.S3[r2(-3)] = s3;  // after k4 read S3[r2(-5)] (same slot)
+                            S.K3[r2(-3)] = rk4_keep3<MODE>(S.K2[r2(-3)], k3);
+                        }
+                        S.S2[r2(-2)] = s2;  // after k3 read S2[r2(-4)] (same slot)
+                        S.K2[r2(-2)] = k2;  // after the final combination read K2[r2(-4)]
+                    }
+                }
+                S.S1[r2(-1)] = s1;  // after k2 read S1[r2(-3)] (same slot)
+            }
+            S.Y[r2(-2)] = i2;  // row Rq-2 is Rq-3 / Rq-4 of the next bodies (its slot held Rq-4, read above)
+        }
+    };
+
+    // One march body at row R: DMA / wait, the y rows from the LDS ring, the steps' stages, and
+    // one stored row (the last step's output, or a dropped store while it is outside the
+    // cone, keeping every body's store pattern the same). KW = warm-up period index (-1 =
+    // steady state): the body's march position is R - R0 = KW kU + P.
+    auto body = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr int KW = decltype(KWc)::value;
+        struct On {
+            constexpr bool operator()(int gs) const { return KW < 0 || KW * kU + P >= 2 * gs; }
+        };
+        constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
+        constexpr auto sl = [](int d) { return ((P + d) % kNR + kNR) % kNR; };  // ring slot of row R+d
+        if constexpr (P % kG == 0) {
+            dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));  // rows R .. R+kG-1 have landed
+        }
+        const V3<T> yR0 = read_row(sl(0)), yR1 = read_row(sl(-1)), yR2 = read_row(sl(-2));
+        // keep the row's DMA at the head of the body: the scheduler would otherwise sink it
+        // below the stencil math, shortening the prefetch distance
+        __builtin_amdgcn_sched_barrier(0);
+        V3<T> o0 = Z;
+        step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o0);
+        if constexpr (NSTEP == 1) {
+            if constexpr (On{}(NST)) store_row(R - NST, o0);
+            else store_row(y0 - 1, Z);
+        } else {
+            // step 2's input rows R-NST (just computed), R-NST-1, R-NST-2 (step 1's ring)
+            const V3<T> i1 = st[0].O[r2(-NST - 1)], i2 = st[0].O[r2(-NST - 2)];
+            if constexpr (On{}(NST)) st[0].O[r2(-NST)] = o0;  // the slot of row R-NST-2, read above
+            V3<T> o1 = Z;
+            step(std::integral_constant<int, 1>{}, Pc, Xc, Yc, On{}, st[1], o0, i1, i2, R - NST, o1);
+            if constexpr (On{}(2 * NST)) store_row(R - 2 * NST, o1);
+            else store_row(y0 - 1, Z);
+        }
+    };
+
+    auto march = [&](auto Xc, auto Yc) {
+        // the kD virtual bodies before R0: DMAs for rows R0 .. R0 + kD - 1 and (dropped)
+        // stores, the same outstanding-op pattern the loop's back edge has
+        [&]<int... Vs>(std::integer_sequence<int, Vs...>) {
+            ([&] {
+                constexpr int v = Vs - kD;  // -kD .. -1
+                if constexpr (((v % kG) + kG) % kG == 0) dma(R0 + v + kD, v + kD);
+                store_row(y0 - 1, Z);
+            }(), ...);
+        }(std::make_integer_sequence<int, kD>{});
+        auto period = [&](auto KWc, int R) {
+            [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+                (body(std::integral_constant<int, Ps>{}, Xc, Yc, KWc, R + Ps), ...);
+            }(std::make_integer_sequence<int, kU>{});
+        };
+        // warm-up periods (R1 - R0 >= kU: at least the first runs), then the steady march
+        [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
+            ([&] {
+                if (Ks == 0 || R0 + Ks * kU < R1) period(std::integral_constant<int, Ks>{}, R0 + Ks * kU);
+            }(), ...);
+        }(std::make_integer_sequence<int, kNW>{});
+        for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
+    };
+    // global edges matter only to strips / segments within kNS cells of them
+    const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - kNS;
+    const bool yclamp = (g.top_clamp && y0 < kNS) || (g.bot_clamp && y1 > g.H - kNS);
+    if (xclamp) {
+        if (yclamp) march(std::true_type{}, std::true_type{});
+        else march(std::true_type{}, std::false_type{});
+    } else {
+        if (yclamp) march(std::false_type{}, std::true_type{});
+        else march(std::false_type{}, std::false_type{});
+    }
+}
+
+}  // namespace
+
+// Launch fused_dppy_kernel<T, nstages, NSTEP, mode> (one translation unit per (T, NSTEP):
+// ws_fused_dppy_<t><n>.hip, compiled in parallel).
+template <typename T, int NSTEP>
+hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
+    const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(kWave);
+#define WS_DPPY_GO(N, M) hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M>), grid, block, 0, s, a, g, nstrips, nsegs)
+#define WS_DPPY_G1(M) WS_DPPY_GO(1, M)
+#define WS_DPPY_G2(M) WS_DPPY_GO(2, M)
+#define WS_DPPY_G4(M) WS_DPPY_GO(4, M)
+    switch (nstages) {
+        case 1: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G1) break;
+        case 2: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G2) break;
+        case 4: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G4) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef WS_DPPY_G1
+#undef WS_DPPY_G2
+#undef WS_DPPY_G4
+#undef WS_DPPY_GO
+    return hipGetLastError();
+}
+
+}  // namespace ws

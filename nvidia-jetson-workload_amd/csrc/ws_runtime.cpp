@@ -24,6 +24,7 @@
 #include "ws_comm.h"
 #include "ws_fused.h"
 #include "ws_halo.h"
+#include "ws_reduce.h"
 #include "ws_ic.h"
 #include "ws_internal.h"
 #include "ws_timer.h"
@@ -253,6 +254,10 @@ struct ws_sim {
     int32_t seg_override = 0; // WS_SEG_ROWS (fixes it)
     bool align = false;       // strip output windows on whole 128-byte lines (WS_ALIGN fixes it)
     bool kernel_fixed = false, seg_fixed = false, align_fixed = false;
+    // time steps per fused launch (temporal blocking; the dppy kernel only): 1, or 2 = two
+    // steps per launch inside run(k) (WS_TB=1|2 fixes it, else the autotuner picks)
+    int32_t tb = 1;
+    bool tb_fixed = false;
     int numerics = WS_NUMERICS_EXACT;  // fused kernels: exact or fast numerics (ws_fused.h)
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
@@ -261,19 +266,25 @@ struct ws_sim {
     // slab decomposition
     ws::SlabComm* comm = nullptr;
     ws::HaloStaging* staging = nullptr;  // slab of a group: its halo messages (group_exchange)
+    uint64_t* cfl_scratch = nullptr;     // ws_sim_cfl: per-level partial maxima + results (device)
+    int64_t cfl_scratch_n = 0;
     int32_t row0 = 0;
 
-    int out_w(int nst) const { return ws::fused_out_w(kernel, nst, (int)elem_size(dtype), align); }
-    int64_t strips(int nst) const { return (slot[0]->W + out_w(nst) - 1) / out_w(nst); }
+    // cone = stages per launch (NST x steps per launch): the strip margins
+    int out_w(int cone) const { return ws::fused_out_w(kernel, cone, (int)elem_size(dtype), align); }
+    int64_t strips(int cone) const { return (slot[0]->W + out_w(cone) - 1) / out_w(cone); }
+    // steps per launch the tuned configuration asks for (1 unless dppy with tb = 2)
+    int launch_tb() const { return kernel == kKernDppLdsY ? tb : 1; }
     // segment rows giving about want_blocks workgroups (at least min_rows rows; the march
     // length rows + 2 NST a multiple of the unroll)
     int32_t seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const {
         const ws_grid* g = slot[0];
-        const int64_t per_seg = strips(nst) * g->L;
+        const int64_t per_seg = strips(nst * launch_tb()) * g->L;
         const int64_t want_segs = std::max<int64_t>(1, (want_blocks + per_seg - 1) / per_seg);
         int64_t rows = (g->H + want_segs - 1) / want_segs;
         rows = std::max<int64_t>(rows, min_rows);
-        rows = (rows + 2 * nst + 7) / 8 * 8 - 2 * nst;
+        const int cone = nst * launch_tb();
+        rows = (rows + 2 * cone + 7) / 8 * 8 - 2 * cone;
         return (int32_t)std::max<int64_t>(1, std::min<int64_t>(rows, g->H));
     }
     // Rows per fused-kernel segment: enough workgroups to fill the chip (64-lane waves of
@@ -343,15 +354,16 @@ struct RowRange {
 // every cross-stream synchronisation: the exchange is stream-ordered on the compute
 // stream (measured on MI355X: two cross-stream event waits per step cost more than an
 // overlapped edge launch saves).
-RowRange step_rows(const ws_sim* s, int nst) {
+RowRange step_rows(const ws_sim* s, int nst, int nsteps = 1) {
     const ws_grid* g = s->slot[0];
-    const int e = (s->block - 1 - s->block_pos) * nst;
+    // a launch of nsteps steps ends on the rows of its last step, block position + nsteps - 1
+    const int e = (s->block - nsteps - s->block_pos) * nst;
     return {g->top_clamp ? 0 : -e, g->bot_clamp ? g->H : g->H + e};
 }
 
 // Launch the fused step kernel over the output rows A U B (segments of seg_rows rows).
 template <typename T>
-void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipStream_t st = nullptr) {
+void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st = nullptr) {
     if (!st) st = s->stream;
     const int nA = (A.rows() + seg_rows - 1) / seg_rows, nB = (B.rows() + seg_rows - 1) / seg_rows;
     if (nA + nB <= 0) return;
@@ -368,7 +380,7 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     a.coriolis_f = (T)s->cfg.coriolis_f;
     a.sp1 = make_spacing<T>(c->dx, c->dy);
     a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
-    a.out_w = s->out_w(nst);
+    a.out_w = s->out_w(nst * nsteps);
     a.seg_rows = seg_rows;
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
@@ -378,9 +390,10 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
     const ws::Geom g = c->geom();
+    if (nsteps > 1 && s->kernel != kKernDppLdsY) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy");
     switch (s->kernel) {
         case kKernX2Y: WS_HIP_CHECK(ws::launch_fused_step_x2y<T>(nst, a, g, st)); break;
-        case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(nst, a, g, st)); break;
+        case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(nst, nsteps, a, g, st)); break;
         default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st)); break;
     }
     ++s->last_launches;
@@ -391,7 +404,7 @@ void fused_launch(ws_sim* s, int nst, RowRange A, RowRange B, int seg_rows, hipS
 //  * slab, fused: start the RCCL halo exchange on the comm stream (after the previous
 //    step's output is complete) and run the interior segments meanwhile.
 template <typename T>
-void step_begin(ws_sim* s) {
+void step_begin(ws_sim* s, int nsteps = 1) {
     ws_grid* c = s->slot[s->cur];
     ws_grid* n = s->slot[1 - s->cur];
     const T dt = (T)s->dt;
@@ -400,12 +413,15 @@ void step_begin(ws_sim* s) {
     const ws::Geom g = c->geom();
     if (use_fused(s)) {
         const int nst = fused_stages(s);
-        s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L, s->stream);
+        // algorithmic bytes of the launch: 6 words per cell-update (read u, v, h + write u, v,
+        // h: the compulsory traffic of one step) x the cell-updates it performs
+        s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L * nsteps, s->stream);
         // slab: at a block start, the block's halo (group slabs: copied by group_step)
         if (s->block_pos == 0 && s->comm) s->comm->exchange(c->f, 3, (int)sizeof(T), g, s->block * nst, s->stream);
-        fused_launch<T>(s, nst, step_rows(s, nst), {0, 0}, s->seg_rows(nst));
+        fused_launch<T>(s, nst, nsteps, step_rows(s, nst, nsteps), {0, 0}, s->seg_rows(nst));
         return;
     }
+    require(nsteps == 1, WS_ERR_INVALID, "multi-step launches need the fused kernels");
     if (method == WS_EULER) {
         launch<T>(s, ws::kAxpy, stage_args<T>(c, c, n, dt, s), c, 0, 6);
     } else if (method == WS_RK2) {
@@ -428,34 +444,66 @@ void step_begin(ws_sim* s) {
 
 // Phase 2: the segments that need the halo (after it arrived), the PE T/P update, and the
 // grid rotation of the reference (current <-> next shared_ptr swap).
+//
+// A two-step launch (temporal blocking) reads the current grid and writes u, v, h two steps
+// on into the next grid; the reference's rotation after two steps puts the current grid
+// back in place, so the u, v, h storage of the two grids is exchanged instead of the slots:
+// the current grid holds the new state and p, T, q are where two rotations leave them. (The
+// intermediate state is never materialised: the non-current grid then holds the state of
+// two steps back instead of one -- visible only through a grid handle held across run(),
+// DESIGN.md deviation D6.)
 template <typename T>
-void step_end(ws_sim* s) {
-    ws_grid* c = s->slot[s->cur];
-    ws_grid* n = s->slot[1 - s->cur];
+void step_end(ws_sim* s, int nsteps = 1) {
     const T dt = (T)s->dt;
     if (use_fused(s)) {
         s->timer.end(s->stream);
-        s->block_pos = (s->block_pos + 1) % s->block;
+        s->block_pos = (s->block_pos + nsteps) % s->block;
     }
-    if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
-        // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
-        // (`dt_ * tendency` has the same operands in every cell: one rounding, done here)
-        const ws::Geom g = c->geom();
-        const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
-        WS_HIP_CHECK(ws::launch_affine2<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], cT,
-                                           (T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], cP, g,
-                                           s->aux_active ? s->aux : s->stream));
-        s->last_launches += 1;
+    for (int i = 0; i < nsteps; ++i) {
+        ws_grid* c = s->slot[(s->cur + i) % 2];
+        ws_grid* n = s->slot[(s->cur + i + 1) % 2];
+        if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
+            // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
+            // (`dt_ * tendency` has the same operands in every cell: one rounding, done here)
+            const ws::Geom g = c->geom();
+            const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
+            WS_HIP_CHECK(ws::launch_affine2<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], cT,
+                                               (T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], cP, g,
+                                               s->aux_active ? s->aux : s->stream));
+            s->last_launches += 1;
+        }
     }
-    s->cur = 1 - s->cur;
+    if (nsteps % 2 == 1) {
+        s->cur = 1 - s->cur;
+    } else {
+        ws_grid* c = s->slot[s->cur];
+        ws_grid* n = s->slot[1 - s->cur];
+        for (int f = 0; f < 3; ++f) {
+            std::swap(c->alloc[f], n->alloc[f]);
+            std::swap(c->f[f], n->f[f]);
+        }
+        n->diag_pending = true;
+    }
     s->slot[s->cur]->diag_pending = true;  // step() ends with calculateDiagnostics (:149)
+}
+
+// Steps the next launch advances, of `remaining`: 2 when the tuned configuration launches
+// two steps at once, the slab block has room for both, and both steps see the config's
+// spacing (the kernel's later stages use it); else 1.
+int launch_steps(const ws_sim* s, int remaining) {
+    if (remaining < 2 || !use_fused(s) || s->launch_tb() < 2) return 1;
+    if (s->nranks > 1 && s->block_pos + 2 > s->block) return 1;  // a slab's block (one domain: no blocks)
+    const double dx = to_prec(s->cfg.dx, s->dtype), dy = to_prec(s->cfg.dy, s->dtype);
+    for (const ws_grid* g : {s->slot[0], s->slot[1]})
+        if (g->dx != dx || g->dy != dy) return 1;
+    return 2;
 }
 
 // One time step on the stream (no host synchronisation).
 template <typename T>
-void enqueue_step(ws_sim* s) {
-    step_begin<T>(s);
-    step_end<T>(s);
+void enqueue_steps(ws_sim* s, int nsteps) {
+    step_begin<T>(s, nsteps);
+    step_end<T>(s, nsteps);
 }
 
 template <typename T>
@@ -492,24 +540,33 @@ void autotune_time(ws_sim* s) {
     struct Cand {
         int kernel, seg;
         bool align;
-        float ms;
+        int tb;
+        float ms;  // per time step
     };
     std::vector<Cand> cands;
     const int fixed_seg = s->seg_override;
-    for (int k : {kKernDppLdsY, kKernX2Y, kKernLds}) {
+    const int fixed_tb = s->tb;
+    // two steps per launch only where a run can use them (slab blocks of >= 2 steps)
+    const bool tb2_ok = s->block >= 2 || s->nranks == 1;
+    for (int k : {kKernDppLdsY, kKernX2Y, kKernLds})
+      for (int tb : {1, 2}) {
+        if (tb == 2 && (k != kKernDppLdsY || !tb2_ok)) continue;
+        if (s->tb_fixed && k == kKernDppLdsY && tb != fixed_tb) continue;
+        s->tb = tb;
+        const int cone = nst * tb;
         for (bool al : {false, true}) {
             if (s->align_fixed && al != s->align) continue;
             s->kernel = k;
-            const bool same = ws::fused_out_w(k, nst, (int)elem_size(s->dtype), true) ==
-                              ws::fused_out_w(k, nst, (int)elem_size(s->dtype), false);
+            const bool same = ws::fused_out_w(k, cone, (int)elem_size(s->dtype), true) ==
+                              ws::fused_out_w(k, cone, (int)elem_size(s->dtype), false);
             if (al && same) continue;  // already aligned
             // aligned windows below 3/4 of the strip waste too much recomputation
-            if (al && 4 * ws::fused_out_w(k, nst, (int)elem_size(s->dtype), true) < 3 * ws::fused_strip_cols(k))
+            if (al && 4 * ws::fused_out_w(k, cone, (int)elem_size(s->dtype), true) < 3 * ws::fused_strip_cols(k))
                 continue;
             const bool save_al = s->align;
             s->align = al;
             if (s->seg_fixed) {
-                cands.push_back({k, fixed_seg, al, 0.f});
+                cands.push_back({k, fixed_seg, al, tb, 0.f});
             } else {
                 // the default, and segment lengths giving whole multiples of the chip's wave
                 // slots (1024 SIMDs; an LDS workgroup is 4 waves) so no SIMD runs a lone
@@ -523,11 +580,11 @@ void autotune_time(ws_sim* s) {
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
-                for (int seg : segs) cands.push_back({k, seg, al, 0.f});
+                for (int seg : segs) cands.push_back({k, seg, al, tb, 0.f});
             }
             s->align = save_al;
         }
-    }
+      }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     WS_HIP_CHECK(hipEventCreate(&e0));
     WS_HIP_CHECK(hipEventCreate(&e1));
@@ -536,14 +593,15 @@ void autotune_time(ws_sim* s) {
         s->kernel = c.kernel;
         s->seg_override = c.seg;
         s->align = c.align;
+        s->tb = c.tb;
         const int H = s->slot[0]->H, seg = s->seg_rows(nst);
         WS_HIP_CHECK(hipEventRecord(e0, s->stream));
-        for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, {0, H}, {0, 0}, seg);
+        for (int i = 0; i < reps; ++i) fused_launch<T>(s, nst, c.tb, {0, H}, {0, 0}, seg);
         WS_HIP_CHECK(hipEventRecord(e1, s->stream));
         WS_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0.f;
         WS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        return ms / reps;
+        return ms / reps / c.tb;
     };
     float first = 0.f;
     for (Cand& c : cands) first += time_cand(c, 1);  // warm-up (code load, clocks)
@@ -556,16 +614,21 @@ void autotune_time(ws_sim* s) {
         for (Cand& c : cands) {
             const float t = time_cand(c, reps);
             c.ms = std::min(c.ms, t);
-            spent += t * reps;
+            spent += t * reps * c.tb;
         }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     const Cand* best = &cands[0];
     for (const Cand& c : cands)
         if (c.ms < best->ms) best = &c;
+    if (env_int("WS_TUNE_LOG", 0))
+        for (const Cand& c : cands)
+            std::fprintf(stderr, "ws autotune: kernel %d tb %d seg %d align %d  %.4f ms/step%s\n", c.kernel, c.tb, c.seg,
+                         (int)c.align, c.ms, &c == best ? "  <- chosen" : "");
     s->kernel = best->kernel;
     s->seg_override = best->seg;
     s->align = best->align;
+    s->tb = best->tb;
     s->last_launches = 0;
 }
 
@@ -579,7 +642,7 @@ struct TuneKey {
     }
 };
 struct TuneChoice {
-    int32_t kernel, seg, align;
+    int32_t kernel, seg, align, tb;
 };
 std::mutex g_tune_mu;
 std::map<TuneKey, TuneChoice> g_tune_cache;
@@ -605,9 +668,10 @@ void tune_file_load_locked() {
     TuneKey k;
     TuneChoice c;
     std::memset(&k, 0, sizeof(k));
-    while (std::fscanf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d", &k.W, &k.H, &k.L, &k.dtype, &k.nst, &k.numerics,
-                       &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg, &c.align) == 13)
-        if (c.kernel == kKernLds || c.kernel == kKernDppLdsY || c.kernel == kKernX2Y) g_tune_cache[k] = c;
+    while (std::fscanf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d", &k.W, &k.H, &k.L, &k.dtype, &k.nst,
+                       &k.numerics, &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg, &c.align, &c.tb) == 14)
+        if ((c.kernel == kKernLds || c.kernel == kKernDppLdsY || c.kernel == kKernX2Y) && (c.tb == 1 || c.tb == 2))
+            g_tune_cache[k] = c;
     std::fclose(f);
 }
 
@@ -615,8 +679,8 @@ void tune_file_append_locked(const TuneKey& k, const TuneChoice& c) {
     const char* path = std::getenv("WS_TUNE_CACHE");
     if (!path) return;
     if (FILE* f = std::fopen(path, "a")) {
-        std::fprintf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d\n", k.W, k.H, k.L, k.dtype, k.nst, k.numerics, k.top,
-                     k.bot, k.block, k.device, c.kernel, c.seg, c.align);
+        std::fprintf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", k.W, k.H, k.L, k.dtype, k.nst, k.numerics,
+                     k.top, k.bot, k.block, k.device, c.kernel, c.seg, c.align, c.tb);
         std::fclose(f);
     }
 }
@@ -636,29 +700,31 @@ void autotune(ws_sim* s) {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             tune_file_load_locked();
             auto it = g_tune_cache.find(key);
-            if (it != g_tune_cache.end() && !s->seg_fixed && !s->align_fixed) {
+            if (it != g_tune_cache.end() && !s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
                 s->kernel = it->second.kernel;
                 s->seg_override = it->second.seg;
                 s->align = it->second.align != 0;
+                s->tb = it->second.tb;
                 hit = true;
             }
         }
         if (!hit) {
             autotune_time<T>(s);
-            if (!s->seg_fixed && !s->align_fixed) {
+            if (!s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
                 std::lock_guard<std::mutex> lk(g_tune_mu);
-                const TuneChoice c{s->kernel, s->seg_override, s->align ? 1 : 0};
+                const TuneChoice c{s->kernel, s->seg_override, s->align ? 1 : 0, s->tb};
                 g_tune_cache[key] = c;
                 tune_file_append_locked(key, c);
             }
         }
     }
     if (s->comm && s->comm->nranks() > 1) {
-        int32_t v[3] = {s->kernel, s->seg_override, s->align ? 1 : 0};
-        s->comm->broadcast_i32(v, 3, 0, s->stream);
+        int32_t v[4] = {s->kernel, s->seg_override, s->align ? 1 : 0, s->tb};
+        s->comm->broadcast_i32(v, 4, 0, s->stream);
         s->kernel = v[0];
         s->seg_override = v[1];
         s->align = v[2] != 0;
+        s->tb = v[3];
     }
 }
 
@@ -692,11 +758,15 @@ void run_steps(ws_sim* s, int k) {
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
     }
-    for (int i = 0; i < k; ++i) {
-        if (s->dtype == WS_F64) enqueue_step<double>(s);
-        else enqueue_step<float>(s);
-        s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
-        s->step++;
+    for (int i = 0; i < k;) {
+        const int n = launch_steps(s, k - i);
+        if (s->dtype == WS_F64) enqueue_steps<double>(s, n);
+        else enqueue_steps<float>(s, n);
+        for (int j = 0; j < n; ++j) {
+            s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
+            s->step++;
+        }
+        i += n;
     }
     if (s->aux_active) {
         WS_HIP_CHECK(hipEventRecord(s->aux_out, s->aux));
@@ -718,7 +788,9 @@ void run_steps(ws_sim* s, int k) {
     WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     if (span) {
         const ws::Geom g = s->slot[0]->geom();
-        s->timer.add_span(0, 6.0 * elem_size(s->dtype) * g.W * g.H * g.L, s->last_launches, ms);
+        // per launch: 6 words per cell-update x the cell-updates of the run / its launches
+        s->timer.add_span(0, 6.0 * elem_size(s->dtype) * g.W * g.H * g.L * k / std::max<int64_t>(1, s->last_launches),
+                          s->last_launches, ms);
         s->timer.suspend(false);
     }
     s->last_ms = ms;
@@ -734,6 +806,7 @@ void sim_free(ws_sim* s) {
         if (e) (void)hipEventDestroy(e);
     if (s->aux) (void)hipStreamDestroy(s->aux);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
+    if (s->cfl_scratch) (void)hipFree(s->cfl_scratch);
     delete s->comm;
     delete s->staging;
     delete s;
@@ -789,6 +862,11 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             s->kernel_fixed = true;
         }
         if (const char* e = std::getenv("WS_WANT_BLOCKS")) s->want_blocks_override = std::atoi(e);
+        if (const char* e = std::getenv("WS_TB")) {
+            s->tb = std::atoi(e);
+            require(s->tb == 1 || s->tb == 2, WS_ERR_INVALID, "WS_TB must be 1 or 2");
+            s->tb_fixed = true;
+        }
         if (const char* e = std::getenv("WS_SEG_ROWS")) {
             s->seg_override = std::atoi(e);
             s->seg_fixed = s->seg_override > 0;
@@ -1428,7 +1506,61 @@ int ws_sim_fused_variant(const ws_sim_t* s, int32_t* kernel, int32_t* seg_rows, 
         const bool fused = use_fused(s);
         if (kernel) *kernel = fused ? s->kernel : -1;
         if (seg_rows) *seg_rows = fused ? s->seg_rows(fused_stages(s)) : 0;
-        if (out_cols) *out_cols = fused ? s->out_w(fused_stages(s)) : 0;
+        if (out_cols) *out_cols = fused ? s->out_w(fused_stages(s) * s->launch_tb()) : 0;
+    });
+}
+
+int ws_sim_cfl(ws_sim_t* s, double* cfl, double* per_level, int32_t nlevels, double* ms) {
+    return guarded([&] {
+        require(s != nullptr && cfl != nullptr, WS_ERR_INVALID, "null pointer");
+        set_device(s->device);
+        const ws_grid* c = s->slot[s->cur];
+        const ws::Geom g = c->geom();
+        require(per_level == nullptr || nlevels >= g.L, WS_ERR_INVALID, "per_level needs num_levels entries");
+        const int64_t need = (int64_t)g.L * (ws::cfl_partials(g) + 1);
+        if (s->cfl_scratch_n < need) {
+            if (s->cfl_scratch) WS_HIP_CHECK(hipFree(s->cfl_scratch));
+            s->cfl_scratch = nullptr;
+            s->cfl_scratch_n = 0;
+            WS_HIP_CHECK(hipMalloc(&s->cfl_scratch, need * sizeof(uint64_t)));
+            s->cfl_scratch_n = need;
+        }
+        uint64_t* out = s->cfl_scratch;
+        uint64_t* partial = s->cfl_scratch + g.L;
+        WS_HIP_CHECK(hipEventRecord(s->ev0, s->stream));
+        auto go = [&](auto tag) {
+            using T = decltype(tag);
+            const T dt = (T)s->dt;
+            WS_HIP_CHECK(ws::launch_cfl<T>((const T*)c->f[WS_FIELD_U], (const T*)c->f[WS_FIELD_V],
+                                           (const T*)c->f[WS_FIELD_H], g, (T)s->cfg.gravity, dt / (T)c->dx,
+                                           dt / (T)c->dy, partial, out, s->stream));
+        };
+        if (s->dtype == WS_F64) go(double{});
+        else go(float{});
+        WS_HIP_CHECK(hipEventRecord(s->ev1, s->stream));
+        // slab decomposition: the per-level maxima over every rank, on the device (RCCL)
+        if (s->comm) s->comm->allreduce_max_u64_device(out, g.L, s->stream);
+        std::vector<uint64_t> bits(g.L);
+        WS_HIP_CHECK(hipMemcpyAsync(bits.data(), out, g.L * sizeof(uint64_t), hipMemcpyDeviceToHost, s->stream));
+        WS_HIP_CHECK(hipStreamSynchronize(s->stream));
+        uint64_t m = 0;
+        for (int l = 0; l < g.L; ++l) {
+            m = std::max(m, bits[l]);
+            if (per_level) std::memcpy(&per_level[l], &bits[l], sizeof(double));
+        }
+        std::memcpy(cfl, &m, sizeof(double));
+        if (ms) {
+            float t = 0.f;
+            WS_HIP_CHECK(hipEventElapsedTime(&t, s->ev0, s->ev1));
+            *ms = t;
+        }
+    });
+}
+
+int ws_sim_steps_per_launch(const ws_sim_t* s, int32_t* steps) {
+    return guarded([&] {
+        require(s != nullptr && steps != nullptr, WS_ERR_INVALID, "null pointer");
+        *steps = use_fused(s) ? s->launch_tb() : 1;
     });
 }
 
@@ -1537,13 +1669,13 @@ void group_exchange(ws_group* gr, int nfields, int depth) {
 }
 
 template <typename T>
-void group_step(ws_group* gr) {
+void group_step(ws_group* gr, int nsteps) {
     ws_sim* s0 = gr->slabs[0];
     if (s0->block_pos == 0) {  // a block starts: the block's halo, by device copies
         group_exchange(gr, 3, s0->block * fused_stages(s0));
     }
-    for (ws_sim* s : gr->slabs) step_begin<T>(s);
-    for (ws_sim* s : gr->slabs) step_end<T>(s);
+    for (ws_sim* s : gr->slabs) step_begin<T>(s, nsteps);
+    for (ws_sim* s : gr->slabs) step_end<T>(s, nsteps);
 }
 
 }  // namespace
@@ -1613,18 +1745,23 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
                 s->kernel = s0->kernel;
                 s->seg_override = s0->seg_override;
                 s->align = s0->align;
+                s->tb = s0->tb;
                 s->tuned = true;
             }
         }
         for (ws_sim* s : gr->slabs) s->block_pos = 0;
         WS_HIP_CHECK(hipEventRecord(s0->ev0, gr->stream));
-        for (int i = 0; i < k; ++i) {
-            if (s0->dtype == WS_F64) group_step<double>(gr);
-            else group_step<float>(gr);
-            for (ws_sim* s : gr->slabs) {
-                s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
-                s->step++;
-            }
+        for (int i = 0; i < k;) {
+            int n = 2;  // every slab must agree (they share the block position and the choice)
+            for (ws_sim* s : gr->slabs) n = std::min(n, launch_steps(s, k - i));
+            if (s0->dtype == WS_F64) group_step<double>(gr, n);
+            else group_step<float>(gr, n);
+            for (ws_sim* s : gr->slabs)
+                for (int j = 0; j < n; ++j) {
+                    s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
+                    s->step++;
+                }
+            i += n;
         }
         WS_HIP_CHECK(hipEventRecord(s0->ev1, gr->stream));
         if (k > 0) {  // seam diagnostics need the neighbours' current rows (see run_steps)

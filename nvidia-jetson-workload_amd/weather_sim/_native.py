@@ -123,6 +123,8 @@ SIGNATURES = {
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
     "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
+    "ws_sim_steps_per_launch": [_P, _PI],
+    "ws_sim_cfl": [_P, _PD, _PD, _I, _PD],
     "ws_sim_set_numerics": [_P, _I],
     "ws_sim_get_numerics": [_P, _PI],
     "ws_slab_exchange_plan": [_I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ws_xfer_t), _I, _PI, _PL, _PL],

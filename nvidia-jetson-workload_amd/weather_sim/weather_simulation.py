@@ -678,6 +678,26 @@ class WeatherSimulation:
         return ({-1: "stage_kernels", 0: "fused_lds", 4: "fused_dppy", 5: "fused_x2y"}[k.value], seg.value,
                 cols.value)
 
+    def get_cfl(self, per_level=False, with_time=False):
+        """Extension: the CFL number max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy)
+        of the current state by a device reduction (ws_hip.h ws_sim_cfl; on a multi-GPU slab a
+        collective over all ranks). per_level=True: (max, per-level array); with_time=True
+        also returns the reduction's device milliseconds."""
+        c, ms = ctypes.c_double(), ctypes.c_double()
+        L = int(self._config_py.num_levels)
+        arr = np.empty(max(1, L), np.float64)
+        check(lib.ws_sim_cfl(self._h, ctypes.byref(c), arr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), arr.size,
+                             ctypes.byref(ms)))
+        out = (c.value, arr) if per_level else c.value
+        return (out, ms.value) if with_time else out
+
+    def steps_per_launch(self):
+        """Extension: time steps one fused launch advances inside run() (1, or 2 with temporal
+        blocking; ws_hip.h ws_sim_steps_per_launch)."""
+        n = ctypes.c_int32()
+        check(lib.ws_sim_steps_per_launch(self._h, ctypes.byref(n)))
+        return n.value
+
     def set_numerics(self, mode):
         """Extension: "exact" (bit-for-bit with the reference) or "fast" (FMA re-association,
         the fp64 default; ws_hip.h WS_NUMERICS_*) for the fused step kernels."""
@@ -897,82 +917,125 @@ class AdaptiveKernelManager:
 
 
 # ---------------------------------------------------------------------------------
-# High-level wrapper (weather_simulation.py:194-371)
+# High-level wrapper and helpers (the reference's weather_simulation.py:194-520)
+#
+# Table-driven: the string-argument maps, the initial-condition parameter lists and the
+# snapshot / device-info layouts are data; the behaviour (defaults, silent fallback for an
+# unknown name, snapshot every output_interval steps, None + a message on a bad IC) is the
+# reference's, pinned by tests/test_gpu_parity.py::test_wrapper_snapshots_and_errors and
+# tests/test_output.py.
 # ---------------------------------------------------------------------------------
+
+# wrapper string arguments -> enum values; an unknown string takes the default, silently
+# (reference :235-269)
+_ENUM_ARGS = {
+    "model": ({"shallow_water": SimulationModel.ShallowWater, "barotropic": SimulationModel.Barotropic,
+               "primitive": SimulationModel.PrimitiveEquations, "general": SimulationModel.General},
+              SimulationModel.ShallowWater),
+    "integration_method": ({"euler": IntegrationMethod.ExplicitEuler, "rk2": IntegrationMethod.RungeKutta2,
+                            "rk4": IntegrationMethod.RungeKutta4, "adams_bashforth": IntegrationMethod.AdamsBashforth,
+                            "semi_implicit": IntegrationMethod.SemiImplicit},
+                           IntegrationMethod.RungeKutta4),
+    "compute_backend": ({"cuda": ComputeBackend.CUDA, "hip": ComputeBackend.CUDA, "cpu": ComputeBackend.CPU,
+                         "hybrid": ComputeBackend.Hybrid, "adaptive": ComputeBackend.AdaptiveHybrid},
+                        ComputeBackend.AdaptiveHybrid),
+}
+
+
+def _enum_arg(field, value):
+    names, default = _ENUM_ARGS[field]
+    return names.get(value.lower(), default) if isinstance(value, str) else value
+
+
+# initial condition name -> (class, constructor parameters as (keyword, default)) --
+# the keywords and defaults create_initial_condition accepts (reference :376-470)
+_IC_TABLE = {
+    "uniform": (UniformInitialCondition, (("u", 0.0), ("v", 0.0), ("h", 10.0), ("p", 1000.0), ("t", 300.0),
+                                          ("q", 0.0))),
+    "random": (RandomInitialCondition, (("seed", 0), ("amplitude", 1.0))),
+    "zonal_flow": (ZonalFlowInitialCondition, (("u_max", 10.0), ("h_mean", 10.0), ("beta", 0.1))),
+    "vortex": (VortexInitialCondition, (("x_center", 0.5), ("y_center", 0.5), ("radius", 0.1), ("strength", 10.0),
+                                        ("h_mean", 10.0))),
+    "jet_stream": (JetStreamInitialCondition, (("y_center", 0.5), ("width", 0.1), ("strength", 10.0),
+                                               ("h_mean", 10.0))),
+    "breaking_wave": (BreakingWaveInitialCondition, (("amplitude", 1.0), ("wavelength", 0.2), ("h_mean", 10.0))),
+    "front": (FrontInitialCondition, (("y_position", 0.5), ("width", 0.05), ("temp_difference", 10.0),
+                                      ("wind_shear", 5.0))),
+    "mountain": (MountainInitialCondition, (("x_center", 0.3), ("y_center", 0.5), ("radius", 0.1), ("height", 1.0),
+                                            ("u_base", 5.0))),
+    "atmospheric_profile": (AtmosphericProfileInitialCondition, (("profile_name", "standard"),)),
+}
+
+# the wrapper's snapshot dict: key -> how to read it from (simulation, current grid)
+_SNAPSHOT = (
+    ("time", lambda sim, g: sim.get_current_time()),
+    ("step", lambda sim, g: sim.get_current_step()),
+    ("u", lambda sim, g: g.get_velocity_field()[0].copy()),
+    ("v", lambda sim, g: g.get_velocity_field()[1].copy()),
+    ("height", lambda sim, g: g.get_height_field().copy()),
+    ("vorticity", lambda sim, g: g.get_vorticity_field().copy()),
+)
+
+
 class WeatherSimulationWrapper:
-    """High-level wrapper for the Weather Simulation."""
+    """High-level wrapper: string arguments, lazy initialisation and periodic snapshots
+    around one WeatherSimulation (same constructor signature and defaults as the reference,
+    plus double_precision / num_levels)."""
 
     def __init__(self, width: int = 256, height: int = 256, model: Union[str, int] = "shallow_water", dt: float = 0.01,
                  integration_method: Union[str, int] = "rk4", backend: Union[str, int] = "adaptive",
                  device_id: int = 0, threads: int = 0, output_interval: int = 10, output_path: str = "./output",
                  double_precision: bool = False, num_levels: int = 1):
-        self.config = SimulationConfig()
-        self.config.grid_width = width
-        self.config.grid_height = height
-        self.config.dt = dt
-        self.config.output_interval = output_interval
-        self.config.output_path = output_path
-        self.config.device_id = device_id
-        self.config.num_threads = threads
-        self.config.double_precision = double_precision
-        self.config.num_levels = num_levels
-        if isinstance(model, str):
-            model_map = {"shallow_water": SimulationModel.ShallowWater, "barotropic": SimulationModel.Barotropic,
-                         "primitive": SimulationModel.PrimitiveEquations, "general": SimulationModel.General}
-            self.config.model = model_map.get(model.lower(), SimulationModel.ShallowWater)
-        else:
-            self.config.model = model
-        if isinstance(integration_method, str):
-            method_map = {"euler": IntegrationMethod.ExplicitEuler, "rk2": IntegrationMethod.RungeKutta2,
-                          "rk4": IntegrationMethod.RungeKutta4, "adams_bashforth": IntegrationMethod.AdamsBashforth,
-                          "semi_implicit": IntegrationMethod.SemiImplicit}
-            self.config.integration_method = method_map.get(integration_method.lower(), IntegrationMethod.RungeKutta4)
-        else:
-            self.config.integration_method = integration_method
-        if isinstance(backend, str):
-            backend_map = {"cuda": ComputeBackend.CUDA, "cpu": ComputeBackend.CPU, "hybrid": ComputeBackend.Hybrid,
-                           "adaptive": ComputeBackend.AdaptiveHybrid, "hip": ComputeBackend.CUDA}
-            self.config.compute_backend = backend_map.get(backend.lower(), ComputeBackend.AdaptiveHybrid)
-        else:
-            self.config.compute_backend = backend
-        self.simulation = WeatherSimulation(self.config)
+        cfg = SimulationConfig()
+        for field, value in (("grid_width", width), ("grid_height", height), ("dt", dt),
+                             ("output_interval", output_interval), ("output_path", output_path),
+                             ("device_id", device_id), ("num_threads", threads),
+                             ("double_precision", double_precision), ("num_levels", num_levels),
+                             ("model", _enum_arg("model", model)),
+                             ("integration_method", _enum_arg("integration_method", integration_method)),
+                             ("compute_backend", _enum_arg("compute_backend", backend))):
+            setattr(cfg, field, value)
+        self.config = cfg
+        self.simulation = WeatherSimulation(cfg)
         self.initialized = False
         self.output_data = []
 
     def set_initial_condition(self, condition_name: str, **kwargs):
-        initial_condition = create_initial_condition(condition_name, **kwargs)
-        if initial_condition:
-            self.simulation.set_initial_condition(initial_condition)
+        ic = create_initial_condition(condition_name, **kwargs)
+        if ic:
+            self.simulation.set_initial_condition(ic)
 
     def initialize(self):
         self.simulation.initialize()
         self.initialized = True
 
-    def step(self):
+    def _ready(self):
         if not self.initialized:
             self.initialize()
+
+    def step(self):
+        self._ready()
         self.simulation.step()
-        if self.config.output_interval > 0 and self.simulation.get_current_step() % self.config.output_interval == 0:
+        every = self.config.output_interval
+        if every > 0 and self.simulation.get_current_step() % every == 0:
             self._store_output()
 
+    def _timed(self, advance, describe):
+        self._ready()
+        t0 = time.time()
+        advance()
+        ms = (time.time() - t0) * 1000
+        _say(describe(ms))
+
     def run(self, steps: int):
-        if not self.initialized:
-            self.initialize()
-        start_time = time.time()
-        self.simulation.run(steps)
-        end_time = time.time()
-        elapsed = (end_time - start_time) * 1000
-        _say(f"Completed {steps} steps in {elapsed:.2f} ms ({elapsed / steps:.2f} ms/step)")
+        self._timed(lambda: self.simulation.run(steps),
+                    lambda ms: f"Completed {steps} steps in {ms:.2f} ms ({ms / steps:.2f} ms/step)")
 
     def run_until(self, max_time: float):
-        if not self.initialized:
-            self.initialize()
-        start_time = time.time()
-        self.simulation.run_until(max_time)
-        end_time = time.time()
-        steps = self.simulation.get_current_step()
-        elapsed = (end_time - start_time) * 1000
-        _say(f"Reached time {max_time} in {elapsed:.2f} ms ({elapsed / steps:.2f} ms/step)")
+        # the per-step figure divides by the simulation's total step count, as the reference does
+        self._timed(lambda: self.simulation.run_until(max_time),
+                    lambda ms: f"Reached time {max_time} in {ms:.2f} ms "
+                               f"({ms / self.simulation.get_current_step():.2f} ms/step)")
 
     def get_grid(self):
         return self.simulation.get_current_grid()
@@ -985,52 +1048,18 @@ class WeatherSimulationWrapper:
 
     def _store_output(self):
         grid = self.simulation.get_current_grid()
-        snapshot = {
-            'time': self.simulation.get_current_time(),
-            'step': self.simulation.get_current_step(),
-            'u': grid.get_velocity_field()[0].copy(),
-            'v': grid.get_velocity_field()[1].copy(),
-            'height': grid.get_height_field().copy(),
-            'vorticity': grid.get_vorticity_field().copy(),
-        }
-        self.output_data.append(snapshot)
+        self.output_data.append({key: read(self.simulation, grid) for key, read in _SNAPSHOT})
 
 
-# ---------------------------------------------------------------------------------
-# Helper functions (weather_simulation.py:376-520)
-# ---------------------------------------------------------------------------------
 def create_initial_condition(name: str, **kwargs) -> Optional[object]:
+    """An initial condition by name with keyword parameters (defaults: _IC_TABLE); other
+    names go to the factory. On failure: a message and None, as the reference."""
     try:
-        if name == "uniform":
-            return UniformInitialCondition(kwargs.get("u", 0.0), kwargs.get("v", 0.0), kwargs.get("h", 10.0),
-                                           kwargs.get("p", 1000.0), kwargs.get("t", 300.0), kwargs.get("q", 0.0))
-        elif name == "random":
-            return RandomInitialCondition(kwargs.get("seed", 0), kwargs.get("amplitude", 1.0))
-        elif name == "zonal_flow":
-            return ZonalFlowInitialCondition(kwargs.get("u_max", 10.0), kwargs.get("h_mean", 10.0),
-                                             kwargs.get("beta", 0.1))
-        elif name == "vortex":
-            return VortexInitialCondition(kwargs.get("x_center", 0.5), kwargs.get("y_center", 0.5),
-                                          kwargs.get("radius", 0.1), kwargs.get("strength", 10.0),
-                                          kwargs.get("h_mean", 10.0))
-        elif name == "jet_stream":
-            return JetStreamInitialCondition(kwargs.get("y_center", 0.5), kwargs.get("width", 0.1),
-                                             kwargs.get("strength", 10.0), kwargs.get("h_mean", 10.0))
-        elif name == "breaking_wave":
-            return BreakingWaveInitialCondition(kwargs.get("amplitude", 1.0), kwargs.get("wavelength", 0.2),
-                                                kwargs.get("h_mean", 10.0))
-        elif name == "front":
-            return FrontInitialCondition(kwargs.get("y_position", 0.5), kwargs.get("width", 0.05),
-                                         kwargs.get("temp_difference", 10.0), kwargs.get("wind_shear", 5.0))
-        elif name == "mountain":
-            return MountainInitialCondition(kwargs.get("x_center", 0.3), kwargs.get("y_center", 0.5),
-                                            kwargs.get("radius", 0.1), kwargs.get("height", 1.0),
-                                            kwargs.get("u_base", 5.0))
-        elif name == "atmospheric_profile":
-            return AtmosphericProfileInitialCondition(kwargs.get("profile_name", "standard"))
-        else:
+        if name not in _IC_TABLE:
             return InitialConditionFactory.get_instance().create_initial_condition(name)
-    except Exception as e:  # reference prints and returns None
+        cls, params = _IC_TABLE[name]
+        return cls(*(kwargs.get(key, default) for key, default in params))
+    except Exception as e:
         print(f"Error creating initial condition '{name}': {e}")
         return None
 
@@ -1039,37 +1068,40 @@ def get_available_initial_conditions() -> List[str]:
     try:
         return InitialConditionFactory.get_instance().get_available_initial_conditions()
     except Exception:
-        return ["uniform", "random", "zonal_flow", "vortex", "jet_stream", "breaking_wave", "front", "mountain",
-                "atmospheric_profile"]
+        return list(_IC_TABLE)
 
 
 def is_cuda_available() -> bool:
-    """True when the HIP device (MI355X) is usable."""
+    """True when the HIP device (MI355X) is usable (the reference's name is kept)."""
     try:
         return AdaptiveKernelManager.get_instance().is_cuda_available()
     except Exception:
         return False
 
 
+_DEVICE_TYPE_NAMES = {DeviceType.Unknown: "Unknown", DeviceType.CPU: "CPU", DeviceType.JetsonOrinNX: "Jetson Orin NX",
+                      DeviceType.T4: "NVIDIA T4", DeviceType.HighEndGPU: "High-End GPU",
+                      DeviceType.OtherGPU: "Other GPU"}
+# get_device_info's keys: key -> how to read it from (capabilities, manager)
+_DEVICE_INFO = (
+    ("device_type", lambda c, m: _DEVICE_TYPE_NAMES.get(c.device_type, "Unknown")),
+    ("device_name", lambda c, m: c.device_name),
+    ("compute_capability", lambda c, m: f"{c.compute_capability_major}.{c.compute_capability_minor}"),
+    ("cuda_cores", lambda c, m: c.cuda_cores),
+    ("multiprocessors", lambda c, m: c.multiprocessors),
+    ("global_memory_mb", lambda c, m: c.global_memory / (1024 * 1024)),
+    ("compute_power_ratio", lambda c, m: c.compute_power_ratio),
+    ("cuda_available", lambda c, m: m.is_cuda_available()),
+    ("arch", lambda c, m: c.arch),
+)
+
+
 def get_device_info() -> Dict:
     try:
         manager = AdaptiveKernelManager.get_instance()
         manager.initialize()
-        capabilities = manager.get_device_capabilities()
-        device_type_map = {DeviceType.Unknown: "Unknown", DeviceType.CPU: "CPU",
-                           DeviceType.JetsonOrinNX: "Jetson Orin NX", DeviceType.T4: "NVIDIA T4",
-                           DeviceType.HighEndGPU: "High-End GPU", DeviceType.OtherGPU: "Other GPU"}
-        return {
-            "device_type": device_type_map.get(capabilities.device_type, "Unknown"),
-            "device_name": capabilities.device_name,
-            "compute_capability": f"{capabilities.compute_capability_major}.{capabilities.compute_capability_minor}",
-            "cuda_cores": capabilities.cuda_cores,
-            "multiprocessors": capabilities.multiprocessors,
-            "global_memory_mb": capabilities.global_memory / (1024 * 1024),
-            "compute_power_ratio": capabilities.compute_power_ratio,
-            "cuda_available": manager.is_cuda_available(),
-            "arch": capabilities.arch,
-        }
+        caps = manager.get_device_capabilities()
+        return {key: read(caps, manager) for key, read in _DEVICE_INFO}
     except Exception as e:
         return {"device_type": "Unknown", "device_name": "Unknown", "error": str(e), "cuda_available": False}
 

@@ -22,6 +22,12 @@
 //   hold                        remember &getCurrentGrid() (stale-handle quirk)
 //   snap <path> | snap_held <path>
 //   time_run <n>                run(n) and print wall seconds (CPU baseline timing)
+//   icband <name> <gW> <gH> <y0:rows,...> <prefix> [p0 p1 ...]
+//                               evaluate IC <name> once on a standalone gW x gH WeatherGrid
+//                               (global coordinates) and write, per band, rows
+//                               [y0, y0 + rows) of u, v, h, p, t, q to
+//                               <prefix>_<y0>_<field>.bin (the input of a band run:
+//                               setfield them into a gW x rows simulation)
 #include "weather_sim/weather_sim.hpp"
 #include "weather_sim/initial_conditions.hpp"
 
@@ -147,6 +153,33 @@ int main(int argc, char** argv) {
         } else if (cmd == "snap_held") {
             std::string p; ss >> p;
             dump(*held, *sim, p);
+        } else if (cmd == "icband") {
+            std::string name, bands, prefix, tok;
+            int gW, gH;
+            ss >> name >> gW >> gH >> bands >> prefix;
+            std::vector<std::string> a;
+            while (ss >> tok) a.push_back(tok);
+            WeatherGrid g(gW, gH);
+            make_ic(name, a)->initialize(g);
+            std::istringstream bs(bands);
+            std::string b;
+            while (std::getline(bs, b, ',')) {
+                const int y0 = std::stoi(b.substr(0, b.find(':'))), rows = std::stoi(b.substr(b.find(':') + 1));
+                if (y0 < 0 || rows <= 0 || y0 + rows > gH) { std::fprintf(stderr, "bad band %s\n", b.c_str()); return 2; }
+                auto band = [&](const std::vector<scalar_t>& v, const char* f) {
+                    const std::string path = prefix + "_" + std::to_string(y0) + "_" + f + ".bin";
+                    FILE* o = std::fopen(path.c_str(), "wb");
+                    if (!o) { std::perror(path.c_str()); std::exit(2); }
+                    std::fwrite(v.data() + (size_t)y0 * gW, sizeof(scalar_t), (size_t)rows * gW, o);
+                    std::fclose(o);
+                };
+                band(g.getVelocityField().u, "u");
+                band(g.getVelocityField().v, "v");
+                band(g.getHeightField().data, "h");
+                band(g.getPressureField().data, "p");
+                band(g.getTemperatureField().data, "t");
+                band(g.getHumidityField().data, "q");
+            }
         } else if (cmd == "time_run") {
             int n; ss >> n;
             auto t0 = std::chrono::steady_clock::now();

@@ -62,10 +62,12 @@ def test_default_numerics_by_precision(monkeypatch):
         s.set_numerics("approximate")
 
 
-@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
-def test_fast_matches_reference_fixtures(kernel, monkeypatch):
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("lds", "1")],
+                         ids=["dppy", "dppy_tb2", "x2y", "lds"])
+def test_fast_matches_reference_fixtures(kernel, tb, monkeypatch):
     monkeypatch.setenv("WS_NUMERICS", "fast")
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     gold = golden("f64")
     n_iso = n_aniso = 0
     worst = 0.0
@@ -98,13 +100,16 @@ def test_fast_matches_reference_fixtures(kernel, monkeypatch):
     print(f"{kernel}: worst relative L2 over {n_iso} fixture cases = {worst:.3e}")
 
 
+@pytest.mark.parametrize("tb", ["1", "2"])
 @pytest.mark.parametrize("method", [0, 1, 2])
-def test_fast_large_grid_vs_oracle(method, monkeypatch):
+def test_fast_large_grid_vs_oracle(method, tb, monkeypatch):
     """4096 x 2048 fp64 (every strip / segment seam of the production tiling), 3 steps,
     f != 0 (the Coriolis instantiation) against the C oracle."""
     from oracle.ws_oracle import OracleSim
 
     monkeypatch.setenv("WS_NUMERICS", "fast")
+    monkeypatch.setenv("WS_KERNEL", "dppy")
+    monkeypatch.setenv("WS_TB", tb)
     W, H, steps = 4096, 2048, 3
     sim = make_sim(W, H, 0, method, True, f=1e-4)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))

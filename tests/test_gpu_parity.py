@@ -56,15 +56,21 @@ def load(sim, s0):
     g.set_humidity_field(s0["q"])
 
 
-KERNELS = [("1", "dppy"), ("1", "x2y"), ("1", "lds"), ("0", "x2y")]
-KERNEL_IDS = ["fused_dppy", "fused_x2y", "fused_lds", "stage_kernels"]
+# (WS_FUSED, WS_KERNEL, WS_TB): every fused variant, dppy also with two steps per launch
+# (temporal blocking: run(n) advances pairs of steps per launch), and the per-stage kernels
+KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "lds", "1"), ("0", "x2y", "1")]
+KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_lds", "stage_kernels"]
+# (kernel, steps per launch) of the fused variants
+FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("lds", "1")]
+FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "lds"]
 
 
-@pytest.mark.parametrize("fused,kernel", KERNELS, ids=KERNEL_IDS)
+@pytest.mark.parametrize("fused,kernel,tb", KERNELS, ids=KERNEL_IDS)
 @pytest.mark.parametrize("variant", ["f32", "f64"])
-def test_stepping_bitwise(variant, fused, kernel, monkeypatch):
+def test_stepping_bitwise(variant, fused, kernel, tb, monkeypatch):
     monkeypatch.setenv("WS_FUSED", fused)
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     gold = golden(variant)
     cases = gold.cases("step/")
     assert len(cases) >= 20
@@ -196,7 +202,10 @@ def test_wrapper_snapshots_and_errors():
     assert m.num_steps == 10 and m.compute_time_ms > 0
 
 
-def test_adapter_and_raw_kernel_abi():
+def test_kernel_adapter_step():
+    """The KernelAdapter plugin API (gpu_adaptability.hpp:242-329): executeShallowWaterStep on
+    two grids == the reference Euler step; the raw-pointer launchers are covered by
+    tests/test_gpu_raw_abi.py."""
     gold = golden("f32")
     s0 = gold.snap("step/m0_i0_jet_stream", "s0")
     s1 = gold.snap("step/m0_i0_jet_stream", "s1")
@@ -224,10 +233,15 @@ def _dam_break(W, H, width_cells, dtype):
     return np.broadcast_to(row, (H, W)).astype(dtype)
 
 
+@pytest.mark.parametrize("tb", ["1", "2"])
 @pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
                                   "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
                                   "C3_zonal_flow_2048_baro_f32"])
-def test_full_size_digests(name):
+def test_full_size_digests(name, tb, monkeypatch):
+    """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size."""
+    if tb == "2":
+        monkeypatch.setenv("WS_KERNEL", "dppy")
+        monkeypatch.setenv("WS_TB", "2")
     d = large_digests()[name]
     spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
     W, H = int(spec["width"]), int(spec["height"])
@@ -253,12 +267,16 @@ def test_full_size_digests(name):
                         f"|ref|={ref_l2!r})")
 
 
-@pytest.mark.parametrize("aux", ["1", "0"])
-def test_pe_levels_match_reference_per_level(aux, monkeypatch):
+@pytest.mark.parametrize("aux,tb", [("1", "0"), ("0", "0"), ("1", "2")])
+def test_pe_levels_match_reference_per_level(aux, tb, monkeypatch):
     """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
     must equal a standalone reference run of that level (bitwise) -- with the T / P update
-    on the second stream (WS_PE_AUX=1, the default) and on the main stream."""
+    on the second stream (WS_PE_AUX=1, the default) and on the main stream, and with two
+    steps per launch (dppy, two T / P updates per launch)."""
     monkeypatch.setenv("WS_PE_AUX", aux)
+    if tb != "0":
+        monkeypatch.setenv("WS_KERNEL", "dppy")
+        monkeypatch.setenv("WS_TB", tb)
     digests = large_digests()
     L = 32
     sim = make_sim(1024, 1024, 2, 2, False, max_time=1e30, levels=L)
@@ -275,17 +293,18 @@ def test_pe_levels_match_reference_per_level(aux, monkeypatch):
             assert _digest(got[f]) == h, (k, f)
 
 
-@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
+@pytest.mark.parametrize("kernel,tb", FUSED, ids=FUSED_IDS)
 @pytest.mark.parametrize("seg_rows", ["0", "5", "33"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, monkeypatch):
+def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, tb, monkeypatch):
     """Strip (x) and segment (y) seams of the fused kernel: 700 x 77 grid spans three
     256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle."""
     from oracle.ws_oracle import OracleSim
 
     monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     W, H = 700, 77
     sim = make_sim(W, H, 0, method, fp64, dx=1.0, dy=2.0, f=0.3)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
@@ -307,9 +326,9 @@ def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, monkeypatch):
 _LARGE_REF = {}
 
 
-@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
+@pytest.mark.parametrize("kernel,tb", FUSED, ids=FUSED_IDS)
 @pytest.mark.parametrize("case", ["rk4_f64", "rk2_f32"])
-def test_every_variant_large_grid_vs_oracle(case, kernel, monkeypatch):
+def test_every_variant_large_grid_vs_oracle(case, kernel, tb, monkeypatch):
     """Every variant pinned at a grid large enough that late-dispatched workgroups run
     beside finished ones (4096 x 2048, segments of 64 rows): a 16-byte store data hazard
     corrupted fused_x2y here and never at the small tiling sizes; bitwise vs the oracle."""
@@ -318,6 +337,7 @@ def test_every_variant_large_grid_vs_oracle(case, kernel, monkeypatch):
     method, fp64 = (2, True) if case == "rk4_f64" else (1, False)
     monkeypatch.setenv("WS_SEG_ROWS", "64")
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     W, H, steps = 4096, 2048, 2
     sim = make_sim(W, H, 0, method, fp64, dx=1.0, dy=1.0, f=1e-4, max_time=1e30)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
@@ -359,15 +379,19 @@ def test_fused_non_pow2_spacing_vs_oracle():
         np.testing.assert_array_equal(got[k], ref.get_field(k), err_msg=k)
 
 
-@pytest.mark.parametrize("kernel,seg_rows", [("dppy", "6"), ("dppy", "0"), ("x2y", "6"), ("x2y", "0"), ("lds", "6"), ("lds", "0")])
+@pytest.mark.parametrize("kernel,seg_rows,tb", [("dppy", "6", "1"), ("dppy", "0", "1"), ("dppy", "6", "2"),
+                                                 ("dppy", "0", "2"), ("x2y", "6", "1"), ("x2y", "0", "1"),
+                                                 ("lds", "6", "1"), ("lds", "0", "1")])
 @pytest.mark.parametrize("nslabs", [2, 3, 5])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_slab_group_matches_single_domain(fp64, method, nslabs, kernel, seg_rows, monkeypatch):
+def test_slab_group_matches_single_domain(fp64, method, nslabs, kernel, seg_rows, tb, monkeypatch):
     """y-slab decomposition (interior segments, halo exchange, edge segments) == one domain,
-    bit-for-bit, for uneven slab heights and several segment sizes."""
+    bit-for-bit, for uneven slab heights and several segment sizes (dppy also with two steps
+    per launch inside the deep-halo blocks)."""
     monkeypatch.setenv("WS_KERNEL", kernel)
     monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
+    monkeypatch.setenv("WS_TB", tb)
     W, H, steps = 300, 83, 7
 
     def cfg():

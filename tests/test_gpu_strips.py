@@ -37,29 +37,34 @@ def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3):
 
 
 @pytest.mark.parametrize("W", [2, 3, 7, 56, 57, 64, 120, 121, 127, 128, 129, 240, 241, 333])
-@pytest.mark.parametrize("kernel", ["dppy", "x2y"])
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1")], ids=["dppy", "dppy_tb2", "x2y"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_strip_widths(W, kernel, method, fp64, monkeypatch):
+def test_strip_widths(W, kernel, tb, method, fp64, monkeypatch):
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     monkeypatch.setenv("WS_SEG_ROWS", "7")
     run_both(W, 29, method, fp64, 5)
 
 
-@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("lds", "1")],
+                         ids=["dppy", "dppy_tb2", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
-def test_non_pow2_spacing(kernel, method, monkeypatch):
+def test_non_pow2_spacing(kernel, tb, method, monkeypatch):
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     run_both(301, 40, method, True, 4, dx=0.75, dy=1.3)
 
 
 @pytest.mark.parametrize("W", [61, 300, 700])
-@pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("lds", "1")],
+                         ids=["dppy", "dppy_tb2", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
-def test_line_aligned_strips(W, kernel, method, fp64, monkeypatch):
+def test_line_aligned_strips(W, kernel, tb, method, fp64, monkeypatch):
     """WS_ALIGN=1: strip output windows cut to whole 128-byte lines (asymmetric margins)."""
     monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
     monkeypatch.setenv("WS_ALIGN", "1")
     monkeypatch.setenv("WS_SEG_ROWS", "9")
     run_both(W, 37, method, fp64, 5)

@@ -10,18 +10,20 @@ mkdir -p "$OUT/pmc"
 CFG=${CFG:-c2}; METHOD=${METHOD:-rk4}; STEPS=${STEPS:-200}; WARM=${WARM:-300}
 timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS --warmup $WARM > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
-read KERN KNAME SEG ALIGN < <(python3 -c "
+read KERN KNAME SEG ALIGN TB < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
-k={'fused_dpp':'dpp','fused_dppdma':'dppdma','fused_dppy':'dppy','fused_x2':'x2','fused_x2y':'x2y','fused_lds':'lds'}.get(d['kernel'],'dpp')
-n={'dpp':'fused_dpp_kernel','dppdma':'fused_dpp_kernel','dppy':'fused_dpp_kernel','x2y':'fused_x2y_kernel','x2':'fused_x2_kernel','lds':'fused_step_kernel'}[k]
+k={'fused_dppy':'dppy','fused_x2y':'x2y','fused_lds':'lds'}.get(d['kernel'],'dppy')
+n={'dppy':'fused_dppy_kernel','x2y':'fused_x2y_kernel','lds':'fused_step_kernel'}[k]
+tb=d.get('steps_per_launch') or 1
 nst={'euler':1,'rk2':2,'rk4':4}['$METHOD']
 nst=2 if nst==4 and '$CFG' in ('c3','c4') else nst
+cone=nst*tb
 g=16//(8 if '$CFG' in ('c2','c5') or '$CFG'.startswith('c2_') else 4)
-margin=(nst+1)//2*2 if k=='x2' else ((nst+g-1)//g*g if k in ('dppdma','dppy','x2y') else nst)
-full={'dpp':64,'dppdma':64,'dppy':64,'x2':128,'x2y':128,'lds':256}[k]-2*margin
-print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0)")
-echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN"
-export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN
+margin=(cone+g-1)//g*g if k in ('dppy','x2y') else cone
+full={'dppy':64,'x2y':128,'lds':256}[k]-2*margin
+print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0, tb)")
+echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN WS_TB=$TB"
+export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN WS_TB=$TB
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
