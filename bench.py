@@ -451,7 +451,8 @@ def main():
                                     f"and writes y_(n+2) once, so its traffic is about half its algorithmic bytes: "
                                     f"dram_gbs is the measured DRAM rate"
                                     if variant != "stage_kernels" else "SURVEY 8(d) stage-kernel words per launch"),
-                     "dram_gbs": traffic / (tot_ms / n * 1e-3) / 1e9 if traffic else None},
+                     "dram_gbs": traffic / (tot_ms / n * 1e-3) / 1e9 if traffic else None,
+                     "dram_frac": traffic / (tot_ms / n * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
         "cfl": {"value": cfl, "reduction_ms": cfl_ms,
                 "gbs": 3 * (8 if conf["fp64"] else 4) * cells / world / (cfl_ms * 1e-3) / 1e9 if cfl_ms > 0 else None,

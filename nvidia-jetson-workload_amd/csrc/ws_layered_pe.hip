@@ -9,11 +9,12 @@
 //     du/dt = -u u_x - v u_y - M_x + f v,  dv/dt = -u v_x - v v_y - M_y - f u,
 //     dh/dt = -(h u)_x - (h v)_y
 //
-// One kernel per RK stage. A 32 x 8 tile of columns plus a 1-column halo computes the
-// Montgomery potential of every column by a vertical scan, chunk by chunk of levels (each
-// chunk's M profiles in LDS), and after each chunk every thread walks its own column through
-// those levels, taking M's horizontal neighbours from LDS and u, v, h's from global memory
-// (L1/L2), and applies the stage update (and the RK4 accumulator) in the same pass.
+// One kernel per RK stage. A kTX x kTY (128 x 4) tile of columns plus a 1-column halo
+// computes the Montgomery potential of every column by a vertical scan, chunk by chunk of
+// levels (each chunk's M profiles, and the h values the scan loaded, in LDS), and after each
+// chunk every thread walks its own column through those levels, taking M's and h's
+// horizontal neighbours from LDS and u's, v's from global memory (L1/L2), and applies the
+// stage update (and the RK4 accumulator) in the same pass.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -51,8 +52,10 @@ __device__ __forceinline__ int wrapi(int i, int n) { return i < 0 ? i + n : (i >
 
 // Levels are processed in chunks of kChunk: the column scan's running state (total
 // thickness, prefix, M of the level above) stays in registers, each chunk's M profile goes
-// to LDS (kChunk x 10 x 34 values: 11 KB fp32), so many workgroups fit a CU and the
-// column walk of one chunk overlaps the other workgroups' loads.
+// to LDS (Ms: kChunk x kCY x kCX = 8 x 6 x 130 values, 25 KB fp32 / 50 KB fp64) next to
+// the chunk's h tile (Hs, the same size with WS_LPE_HLDS): 50 KB fp32 lets 3 workgroups
+// share a CU (160 KB of LDS), the fp64 kernel's 100 KB one; the column walk of one chunk
+// overlaps the other workgroups' loads.
 #ifndef WS_LPE_CHUNK
 #define WS_LPE_CHUNK 8
 #endif
@@ -65,6 +68,11 @@ constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
 #ifndef WS_LPE_HLDS
 #define WS_LPE_HLDS 1  // the walk takes h's neighbours from an LDS copy of the scan's loads (0: from L1/L2; c4p 20.5 -> 21.2 Gcell/s)
 #endif
+#define WS_LPE_HLDS_ON (WS_LPE_HLDS ? 1 : 0)
+// static LDS of the stage kernel (Ms, and Hs with WS_LPE_HLDS) must fit the CDNA4 CU's 160 KB
+template <typename T>
+constexpr int lpe_lds_bytes() { return (1 + WS_LPE_HLDS_ON) * kChunk * kCY * kCX * (int)sizeof(T); }
+static_assert(lpe_lds_bytes<double>() <= 160 * 1024, "layered PE tile + chunk exceed the gfx950 LDS (160 KB)");
 #ifndef WS_LPE_WAVES
 #define WS_LPE_WAVES 6  // fp32: VGPRs capped at 80 -> 6 waves/SIMD (128x4 tile: 18.5 -> 19.1-19.3 Gcell/s; 8 waves spills: 14.5); fp64 unconstrained
 #endif

@@ -52,6 +52,22 @@ def test_matches_oracle_fp64(W, H, L, method):
     assert m.get_current_step() == 10
 
 
+@pytest.mark.parametrize("W,H,L", [(300, 37, 11), (257, 13, 19), (512, 9, 8)])
+@pytest.mark.parametrize("fp64", [True, False])
+def test_multi_tile_widths_and_partial_chunks(W, H, L, fp64):
+    """Several 128-column tiles in x (the tile-to-tile halo, the periodic wrap across tiles,
+    the LDS h-neighbour path at tile seams), widths that are not a multiple of the tile, and
+    level counts that leave a partial chunk of WS_LPE_CHUNK (8) levels; RK4, fp64 against the
+    fp64 oracle, fp32 against the float32 oracle."""
+    m = model(W, H, L, 2, fp64, dx=1000.0, dy=1300.0)
+    s0 = perturbed(L, H, W, W * L)
+    m.set_state(*s0)
+    m.run(6)
+    want = lp.run(s0, 6, 5.0, 1000.0, 1300.0, G, GP, 1e-4, 2, dtype=np.float64 if fp64 else np.float32)
+    for got, w in zip(m.get_state(), want):
+        assert rel(got, w.astype(np.float64)) < (1e-13 if fp64 else 1e-5)
+
+
 @pytest.mark.parametrize("method", [0, 2])
 def test_matches_oracle_fp32(method):
     W, H, L = 96, 64, 8
