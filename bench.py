@@ -217,7 +217,7 @@ def bench_bvort(args, conf, method, world):
         "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": 1,
                    "integrator": args.method, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _step_traffic(args, launches / args.steps),
                      "kernel": "whole step (LDS-FFT Poisson: bv_rowfft_fwd + bv_colsolve + bv_rowfft_inv, then bv_stage_kernel)",
                      "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
                      "note": "device time of the run (hipEvents on the model's stream) per step; "
@@ -238,16 +238,19 @@ def bench_bvort(args, conf, method, world):
     print(json.dumps(result), flush=True)
 
 
-def _lpe_step_traffic(args, stage_launches_per_step):
-    """HBM bytes per layered-PE step from rocprofv3 PMC (profiles/traffic_c4p_<method>.json,
-    tools/traffic.py: 2 x FETCH_SIZE + WRITE_SIZE per stage-kernel dispatch) x stage launches
-    per step; None when no PMC summary for this config is committed."""
+def _step_traffic(args, stage_launches_per_step):
+    """HBM bytes per physics-mode step from rocprofv3 PMC (profiles/traffic_<config>_<method>.json):
+    "step" = the bytes of every kernel of a step (tools/traffic_step.py), or "kind0" = bytes
+    per stage-kernel dispatch (tools/traffic.py) x stage launches per step; None when no PMC
+    summary for this config is committed."""
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
     if not os.path.exists(tfile):
         return None
     with open(tfile) as f:
-        per_dispatch = json.load(f).get("kind0")
-    return None if per_dispatch is None else per_dispatch * stage_launches_per_step
+        t = json.load(f)
+    if "step" in t:
+        return t["step"]
+    return None if t.get("kind0") is None else t["kind0"] * stage_launches_per_step
 
 
 def lpe_words_per_cell(method):
@@ -311,7 +314,7 @@ def bench_lpe(args, conf, method, world):
         "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": L,
                    "integrator": args.method, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _lpe_step_traffic(args, launches / args.steps),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _step_traffic(args, launches / args.steps),
                      "kernel": "lpe_stage_kernel (whole step)",
                      "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
                      "note": "device time of the run (hipEvents on the model's stream) per step; "

@@ -1,13 +1,13 @@
 #!/bin/bash
 # Round profile of the bench workload: bench (autotuned) -> rocprofv3 kernel-trace stats and
 # PMC passes with the variant the autotuner chose pinned (so every profiled dispatch of the
-# kernel is the measured one) -> traffic JSON. Outputs under gpurun_out/round/.
+# kernel is the measured one) -> traffic JSON. Outputs under gpurun_out/round_<cfg>_<method>/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
-OUT=$R/gpurun_out/round
-mkdir -p "$OUT/pmc"
 CFG=${CFG:-c2}; METHOD=${METHOD:-rk4}; STEPS=${STEPS:-200}; WARM=${WARM:-300}
+OUT=$R/gpurun_out/round_${CFG}_${METHOD}
+mkdir -p "$OUT/pmc"
 timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS --warmup $WARM > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
 read KERN KNAME SEG ALIGN TB < <(python3 -c "
