@@ -59,9 +59,11 @@ hipError_t launch_diagnostics(const T* u, const T* v, T* vort, T* div, const Spa
 // out = in + c * tend_const   (PE T/P stale-tendency update, weather_simulation.cpp:201-214)
 template <typename T>
 hipError_t launch_affine(T* out, const T* in, T c, T tend, const Geom& g, hipStream_t s);
-// both PE updates in one pass: oT = iT + cT, oP = iP + cP (cX = dt * tendency, rounded in T)
+// both PE updates in one pass: oT = iT + cT, oP = iP + cP (cX = dt * tendency, rounded in T);
+// nrep > 1 applies nrep steps' updates in one pass, each rounded: oT = ((iT + cT) + cT) ...
 template <typename T>
-hipError_t launch_affine2(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP, const Geom& g, hipStream_t s);
+hipError_t launch_affine2(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP, const Geom& g, hipStream_t s,
+                          int nrep = 1);
 
 // fill all rows [0,H) of all levels with value
 template <typename T>

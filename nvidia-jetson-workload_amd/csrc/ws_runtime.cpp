@@ -446,11 +446,12 @@ void step_begin(ws_sim* s, int nsteps = 1) {
 // grid rotation of the reference (current <-> next shared_ptr swap).
 //
 // A two-step launch (temporal blocking) reads the current grid and writes u, v, h two steps
-// on into the next grid; the reference's rotation after two steps puts the current grid
-// back in place, so the u, v, h storage of the two grids is exchanged instead of the slots:
-// the current grid holds the new state and p, T, q are where two rotations leave them. (The
-// intermediate state is never materialised: the non-current grid then holds the state of
-// two steps back instead of one -- visible only through a grid handle held across run(),
+// on into the next grid (PE: one T / P pass applies both steps' updates, also into the next
+// grid); the reference's rotation after two steps puts the current grid back in place, so
+// the storage of those fields is exchanged between the two grids instead of the slots: the
+// current grid holds the new state and the other fields are where two rotations leave them.
+// (The intermediate state is never materialised: the non-current grid then holds the state
+// of two steps back instead of one -- visible only through a grid handle held across run(),
 // DESIGN.md deviation D6.)
 template <typename T>
 void step_end(ws_sim* s, int nsteps = 1) {
@@ -459,26 +460,27 @@ void step_end(ws_sim* s, int nsteps = 1) {
         s->timer.end(s->stream);
         s->block_pos = (s->block_pos + nsteps) % s->block;
     }
-    for (int i = 0; i < nsteps; ++i) {
-        ws_grid* c = s->slot[(s->cur + i) % 2];
-        ws_grid* n = s->slot[(s->cur + i + 1) % 2];
-        if (s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS) {
-            // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
-            // (`dt_ * tendency` has the same operands in every cell: one rounding, done here)
-            const ws::Geom g = c->geom();
-            const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
-            WS_HIP_CHECK(ws::launch_affine2<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], cT,
-                                               (T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], cP, g,
-                                               s->aux_active ? s->aux : s->stream));
-            s->last_launches += 1;
-        }
+    ws_grid* c = s->slot[s->cur];
+    ws_grid* n = s->slot[1 - s->cur];
+    const bool pe = s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS;
+    if (pe) {
+        // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
+        // (`dt_ * tendency` has the same operands in every cell: one rounding, done here);
+        // all nsteps updates in one pass, each rounded as the reference rounds it
+        const ws::Geom g = c->geom();
+        const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
+        WS_HIP_CHECK(ws::launch_affine2<T>((T*)n->f[WS_FIELD_T], (const T*)c->f[WS_FIELD_T], cT,
+                                           (T*)n->f[WS_FIELD_P], (const T*)c->f[WS_FIELD_P], cP, g,
+                                           s->aux_active ? s->aux : s->stream, nsteps));
+        s->last_launches += 1;
     }
     if (nsteps % 2 == 1) {
         s->cur = 1 - s->cur;
     } else {
-        ws_grid* c = s->slot[s->cur];
-        ws_grid* n = s->slot[1 - s->cur];
-        for (int f = 0; f < 3; ++f) {
+        // two steps: exchange the storage of the fields written into the next grid (u, v, h
+        // and, for PE, T and P), so the current grid holds the new state
+        for (int f : {WS_FIELD_U, WS_FIELD_V, WS_FIELD_H, WS_FIELD_T, WS_FIELD_P}) {
+            if (!pe && (f == WS_FIELD_T || f == WS_FIELD_P)) continue;
             std::swap(c->alloc[f], n->alloc[f]);
             std::swap(c->f[f], n->f[f]);
         }
