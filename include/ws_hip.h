@@ -229,7 +229,7 @@ int ws_group_run(ws_group_t* group, int32_t num_steps, int32_t* steps_taken);
 /* The halo exchange plan of rank `rank` (new; the reference has no distributed path): the
  * byte ranges a slab's exchange of `depth` rows of `nfields` level-stacked fields moves.
  * Offsets are relative to a field's row 0 of level 0 in the slab-grid layout (`pitch`
- * elements per row, `level_stride` elements per level, 12 halo rows above and below each
+ * elements per row, `level_stride` elements per level, 24 halo rows above and below each
  * level). Per neighbour there is ONE message: its send segments (kind 0) concatenated in
  * plan order (field-major, then level; msg_offset = position in the message), received
  * into the receive segments (kind 1) in the same order. ws_sim_create_slab's RCCL exchange

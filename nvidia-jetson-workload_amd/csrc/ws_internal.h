@@ -9,9 +9,9 @@
 
 namespace ws {
 
-// Halo rows allocated above and below every field: a slab exchanges up to 3 time steps'
-// worth of RK4 dependency cone (3 x 4 rows) at once (see ws_runtime.cpp, slab blocks).
-constexpr int kHalo = 12;
+// Halo rows allocated above and below every field: a slab exchanges up to 6 time steps'
+// worth of RK4 dependency cone (6 x 4 rows) at once (see ws_runtime.cpp, slab blocks).
+constexpr int kHalo = 24;
 
 enum StageMode : int {
     kAxpy = 0,       // out = base + c * k(in)                         (Euler, RK2, RK4 stage 1)

@@ -883,10 +883,12 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         if (slab.nranks > 1 && s->fused) {
             // steps per exchange: as many as the halo (kHalo rows) and the thinnest slab
             // (floor(H / nranks) rows, the same on every rank: neighbours must agree) allow,
-            // at most 3 (the extended-row overhead grows with the square of the block)
+            // at most 6: an exchange is a fixed RCCL latency (~10 us) plus the transfer, the
+            // extended rows cost (block - 2) NST rows per side and launch (C2 at 8 slabs,
+            // block 6: 3 % more rows computed, one exchange per 6 steps instead of 3)
             const int nst = method == WS_EULER ? 1 : method == WS_RK2 ? 2 : 4;
             const int thin = cfg->grid_height / slab.nranks;
-            s->block = std::max(1, std::min(3, std::min(ws::kHalo, thin) / nst));
+            s->block = std::max(1, std::min(6, std::min(ws::kHalo, thin) / nst));
             if (const char* e = std::getenv("WS_SLAB_BLOCK")) s->block = std::max(1, std::min(s->block, std::atoi(e)));
         }
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);

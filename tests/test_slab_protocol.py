@@ -208,7 +208,8 @@ def test_exchange_plan_layout():
         es = 8 if fp64 else 4
         plan, pitch, lstride = _native.exchange_plan(4000, rows, L, fp64, 1, 3, 3, depth)
         row = pitch * es
-        assert pitch % 64 == 0 and pitch >= 4000 and lstride == (rows + 24) * pitch
+        halo2 = lstride // pitch - rows  # halo rows above + below
+        assert pitch % 64 == 0 and pitch >= 4000 and lstride % pitch == 0 and halo2 % 2 == 0 and halo2 // 2 >= depth
         for peer, send_row, recv_row in ((0, 0, -depth), (2, rows - depth, rows)):
             for kind, r0 in ((0, send_row), (1, recv_row)):
                 seg = [x for x in plan if x.peer == peer and x.kind == kind]
@@ -220,8 +221,11 @@ def test_exchange_plan_layout():
         assert {x.peer for x in _native.exchange_plan(64, rows, L, fp64, 0, 3, 3, depth)[0]} == {1}
         assert {x.peer for x in _native.exchange_plan(64, rows, L, fp64, 2, 3, 3, depth)[0]} == {1}
         assert _native.exchange_plan(64, rows, L, fp64, 0, 1, 3, depth)[0] == []
+    _, pitch, lstride = _native.exchange_plan(64, 64, 1, True, 0, 2, 3, 1)
+    halo = (lstride // pitch - 64) // 2
+    _native.exchange_plan(64, 64, 1, True, 0, 2, 3, halo)  # the whole halo
     with pytest.raises(ValueError):
-        _native.exchange_plan(64, 8, 1, True, 0, 2, 3, 13)  # deeper than the 12 halo rows
+        _native.exchange_plan(64, 64, 1, True, 0, 2, 3, halo + 1)  # deeper than the halo rows
 
 
 def test_halo_depth_is_necessary():
