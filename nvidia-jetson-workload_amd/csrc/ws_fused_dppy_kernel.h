@@ -42,12 +42,12 @@ constexpr int kWave = 64;
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
 // XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
 // the neighbour index to the cell itself (weather_simulation.cpp:510-513).
+// l / r: the mid row's left / right neighbours (DPP lane shifts, or LDS reads: see
+// kLdsStages below).
 template <int MODE, bool XCLAMP, bool YCLAMP, typename T>
-__device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
-                                            const V3<T>& mid, const V3<T>& down, const Spacing<T>& sp, T grav,
-                                            T cor) {
-    V3<T> l{from_left(mid.u), from_left(mid.v), from_left(mid.h)};
-    V3<T> r{from_right(mid.u), from_right(mid.v), from_right(mid.h)};
+__device__ __forceinline__ V3<T> stage_tend_lr(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
+                                               const V3<T>& mid, const V3<T>& down, V3<T> l, V3<T> r,
+                                               const Spacing<T>& sp, T grav, T cor) {
     if constexpr (XCLAMP) {
         l = V3<T>{xlo ? mid.u : l.u, xlo ? mid.v : l.v, xlo ? mid.h : l.h};
         r = V3<T>{xhi ? mid.u : r.u, xhi ? mid.v : r.v, xhi ? mid.h : r.h};
@@ -62,6 +62,22 @@ __device__ __forceinline__ V3<T> stage_tend(bool xlo, bool xhi, int j, const Geo
         return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
     }
 }
+
+template <typename T>
+__device__ __forceinline__ V3<T> dpp_left(const V3<T>& m) { return V3<T>{from_left(m.u), from_left(m.v), from_left(m.h)}; }
+template <typename T>
+__device__ __forceinline__ V3<T> dpp_right(const V3<T>& m) { return V3<T>{from_right(m.u), from_right(m.v), from_right(m.h)}; }
+
+// Stages of the launch's cone (bit gs - 1 for stage gs = q NST + s) that take their
+// horizontal neighbours from LDS instead of DPP lane shifts: an fp64 neighbour is two 32-bit
+// DPP moves (VALU), an LDS read is not VALU. Stage 1's mid row is already in the LDS-DMA
+// ring (two extra ds_read per field); a later stage's mid row is the previous body's output
+// of the stage before, which that body writes to a per-wave LDS row (double-buffered by body
+// parity: three ds_write + six ds_read per stage and body). LDS bandwidth and capacity bound
+// how many stages can move (measured).
+#ifndef WS_DPPY_LDSX
+#define WS_DPPY_LDSX 0x1
+#endif
 
 // s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
 // lgkmcnt[11:8], vmcnt[15:14]); the other counters at their maxima = not waited on
@@ -94,6 +110,11 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     // drop below the threshold while the group is still in flight (seen as stale rows at
     // 4096^2). Loads complete in order.
     constexpr int kWaitN = 3 * (kD / kG);
+    constexpr unsigned kLdsX = (unsigned)(WS_DPPY_LDSX) & ((1u << kNS) - 1u);
+    constexpr auto ldsx = [](int gs) { return ((kLdsX >> (gs - 1)) & 1u) != 0; };
+    // LDS row slots of the stages (other than stage 1) that read neighbours from LDS
+    constexpr auto xslot = [](int gs) { return __builtin_popcount(kLdsX & ((1u << (gs - 1)) - 1u) & ~1u); };
+    constexpr int kNX = __builtin_popcount(kLdsX & ~1u);
 
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
@@ -159,6 +180,40 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
         lds_dma16(rh, &ring[2][slot][0], vo);
     };
     auto read_row = [&](int slot) -> V3<T> { return V3<T>{ring[0][slot][lane], ring[1][slot][lane], ring[2][slot][lane]}; };
+    // a ring row's neighbours: lanes 0 / 63 read past the row (the previous / next slot, or
+    // outside the array: LDS returns 0) -- margin lanes only
+    auto ring_left = [&](int slot) -> V3<T> {
+        return V3<T>{ring[0][slot][lane - 1], ring[1][slot][lane - 1], ring[2][slot][lane - 1]};
+    };
+    auto ring_right = [&](int slot) -> V3<T> {
+        return V3<T>{ring[0][slot][lane + 1], ring[1][slot][lane + 1], ring[2][slot][lane + 1]};
+    };
+    // per-wave LDS rows of the LDS-neighbour stages: xrow[parity][slot][field][lane]
+    __shared__ T xrow[2][kNX > 0 ? kNX : 1][3][kWave];
+    auto xput = [&](auto Pc, auto GSc, const V3<T>& v) {
+        constexpr int P = decltype(Pc)::value, gs = decltype(GSc)::value;
+        if constexpr (gs > 1 && ldsx(gs)) {
+            auto& b = xrow[P % 2][xslot(gs)];
+            b[0][lane] = v.u;
+            b[1][lane] = v.v;
+            b[2][lane] = v.h;
+        }
+    };
+    // neighbours of stage gs's mid row `mid` (its ring slot `rs` for stage 1)
+    auto nbrs = [&](auto Pc, auto GSc, const V3<T>& mid, int rs, V3<T>& l, V3<T>& r) {
+        constexpr int P = decltype(Pc)::value, gs = decltype(GSc)::value;
+        if constexpr (!ldsx(gs)) {
+            l = dpp_left(mid);
+            r = dpp_right(mid);
+        } else if constexpr (gs == 1) {
+            l = ring_left(rs);
+            r = ring_right(rs);
+        } else {
+            auto& b = xrow[(P + 1) % 2][xslot(gs)];
+            l = V3<T>{b[0][lane - 1], b[1][lane - 1], b[2][lane - 1]};
+            r = V3<T>{b[0][lane + 1], b[1][lane + 1], b[2][lane + 1]};
+        }
+    };
 
     const V3<T> Z{T(0), T(0), T(0)};
     StepRings<T> st[NSTEP];
@@ -184,31 +239,50 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
         constexpr bool YC = decltype(Yc)::value;
         constexpr auto on = [](int s) { return decltype(ONc){}(q * NST + s); };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
+        auto gsc = [](auto sc) { return std::integral_constant<int, q * NST + decltype(sc)::value>{}; };
+        using S1c = std::integral_constant<int, 1>;
+        using S2c = std::integral_constant<int, 2>;
+        using S3c = std::integral_constant<int, 3>;
+        using S4c = std::integral_constant<int, 4>;
+        constexpr int rs1 = ((P - 1) % kNR + kNR) % kNR;  // ring slot of row R-1 (step 1's stage-1 mid)
+        // stage 1's mid row next body (written even while stage 1 is outside the cone: the
+        // next body may need it)
+        xput(Pc, gsc(S1c{}), i0);
         if constexpr (on(1)) {
             // stage 1 of the launch reads the current grid (its spacing sp1); every later stage
             // a temp / next grid (the config's spacing sp2; the host launches two steps at once
             // only when sp1 == sp2)
             const Spacing<T>& sp_in = q == 0 ? a.sp1 : a.sp2;
-            const V3<T> k1 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 1, g, i2, i1, i0, sp_in, a.gravity, a.coriolis_f);
+            V3<T> l, r;
+            nbrs(Pc, gsc(S1c{}), i1, rs1, l, r);
+            const V3<T> k1 =
+                stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 1, g, i2, i1, i0, l, r, sp_in, a.gravity, a.coriolis_f);
             if constexpr (NST == 1) {
                 out = axpy<MODE>(i1, a.c_dt, k1);  // Euler: y + dt k
             } else {
                 const V3<T> s1 = axpy<MODE>(i1, a.c_half, k1);  // y + (0.5f dt) k
+                xput(Pc, gsc(S2c{}), s1);
                 if constexpr (on(2)) {
-                    const V3<T> k2 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
-                                                              a.sp2, a.gravity, a.coriolis_f);
+                    nbrs(Pc, gsc(S2c{}), S.S1[r2(-2)], 0, l, r);
+                    const V3<T> k2 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
+                                                                 l, r, a.sp2, a.gravity, a.coriolis_f);
                     if constexpr (NST == 2) {
                         out = axpy<MODE>(i2, a.c_dt, k2);  // RK2: y + dt k2
                     } else {
                         const V3<T> s2 = axpy<MODE>(i2, a.c_half, k2);
+                        xput(Pc, gsc(S3c{}), s2);
                         if constexpr (on(3)) {
-                            const V3<T> k3 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 3, g, S.S2[r2(-4)], S.S2[r2(-3)],
-                                                                      s2, a.sp2, a.gravity, a.coriolis_f);
+                            nbrs(Pc, gsc(S3c{}), S.S2[r2(-3)], 0, l, r);
+                            const V3<T> k3 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 3, g, S.S2[r2(-4)],
+                                                                         S.S2[r2(-3)], s2, l, r, a.sp2, a.gravity,
+                                                                         a.coriolis_f);
                             const V3<T> s3 = axpy<MODE>(S.Y[r2(-3)], a.c_dt, k3);
+                            xput(Pc, gsc(S4c{}), s3);
                             if constexpr (on(4)) {
-                                const V3<T> k4 = stage_tend<MODE, XC, YC>(xlo, xhi, Rq - 4, g, S.S3[r2(-5)],
-                                                                          S.S3[r2(-4)], s3, a.sp2, a.gravity,
-                                                                          a.coriolis_f);
+                                nbrs(Pc, gsc(S4c{}), S.S3[r2(-4)], 0, l, r);
+                                const V3<T> k4 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 4, g, S.S3[r2(-5)],
+                                                                             S.S3[r2(-4)], s3, l, r, a.sp2, a.gravity,
+                                                                             a.coriolis_f);
                                 // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
                                 out = rk4_final<MODE>(S.Y[r2(-4)], a.c_dt6, k4, S.K2[r2(-4)], S.K3[r2(-4)]);
                             }
