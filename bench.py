@@ -411,6 +411,7 @@ def main():
     value = cells * args.steps / elapsed
     # CFL of the final state by the device max-reduction (outside the timed region; a
     # collective over the ranks of a slab decomposition, so every rank calls it)
+    sim.get_cfl()  # first call: HIP loads the reduction kernels' code lazily
     cfl, cfl_ms = sim.get_cfl(with_time=True)
     stats = sim.kernel_timing()
     variant, seg_rows, out_cols = sim.fused_variant()

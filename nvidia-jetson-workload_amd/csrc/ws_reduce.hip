@@ -55,22 +55,52 @@ __device__ __forceinline__ uint64_t block_max_u64(uint64_t v) {
     return m;
 }
 
+// per-cell CFL value as the bits of a double (T arithmetic, NaN-propagating max of the two)
+template <typename T>
+__device__ __forceinline__ uint64_t cfl_bits(T u, T v, T h, T gravity, T cx, T cy) {
+    const T c = sqrt(gravity * h);
+    const T a = (fabs(u) + c) * cx;
+    const T b = (fabs(v) + c) * cy;
+    return (uint64_t)__double_as_longlong((double)(a >= b || a != a ? a : b));
+}
+
+// Workgroup (b, level) reduces rows b, b + gridDim.x, ... of one level. A row is read in
+// 16-byte vectors (rows are padded to 64 elements, so they are whole vectors; lanes past W
+// are masked), kUnroll independent vector triples in flight per thread.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void cfl_partial_kernel(const T* __restrict__ u, const T* __restrict__ v,
                                                               const T* __restrict__ h, Geom g, T gravity, T cx, T cy,
                                                               uint64_t* __restrict__ partial) {
+    constexpr int VW = 16 / (int)sizeof(T);
+    constexpr int kUnroll = 4;
+    using V = T __attribute__((ext_vector_type(VW)));
     const int level = blockIdx.y;
     const int64_t lofs = (int64_t)level * g.lstride;
+    const int nvec = (int)(g.pitch / VW);
     uint64_t m = 0;
     for (int y = blockIdx.x; y < g.H; y += gridDim.x) {
         const int64_t row = lofs + (int64_t)y * g.pitch;
-        for (int x = threadIdx.x; x < g.W; x += kThreads) {
-            const T c = sqrt(gravity * h[row + x]);
-            const T a = (fabs(u[row + x]) + c) * cx;
-            const T b = (fabs(v[row + x]) + c) * cy;
-            // NaN-propagating max of the two (a NaN wins via its bit pattern below)
-            const double d = (double)(a >= b || a != a ? a : b);
-            m = umax64(m, (uint64_t)__double_as_longlong(d));
+        const V* U = (const V*)(u + row);
+        const V* Vv = (const V*)(v + row);
+        const V* Hh = (const V*)(h + row);
+        for (int x0 = threadIdx.x; x0 < nvec; x0 += kThreads * kUnroll) {
+            V uu[kUnroll], vv[kUnroll], hh[kUnroll];
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                const int xv = x0 + k * kThreads;
+                if (xv < nvec) {
+                    uu[k] = U[xv];
+                    vv[k] = Vv[xv];
+                    hh[k] = Hh[xv];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) {
+                const int xv = x0 + k * kThreads;
+#pragma unroll
+                for (int j = 0; j < VW; ++j)
+                    if (xv < nvec && xv * VW + j < g.W) m = umax64(m, cfl_bits<T>(uu[k][j], vv[k][j], hh[k][j], gravity, cx, cy));
+            }
         }
     }
     m = block_max_u64(m);

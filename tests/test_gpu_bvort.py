@@ -142,3 +142,18 @@ def test_poisson_lds_fft_fp32(W, H):
     assert rel(m.get_streamfunction(), bo.poisson(z0, 1.0, 1.0)) < 1e-5
     m.run(5)
     assert rel(m.get_vorticity_field(), bo.run(z0, 5, dt, 1.0, 1.0, 0.2, 0.01, 2)) < 1e-4
+
+
+def test_bench_size_c3p_vs_oracle():
+    """The bench workload itself (config c3p: 2048^2 fp32 RK4, two Rossby modes, dt 0.05,
+    beta 1e-3, nu 0.01 -- bench.py bench_bvort) for 2 steps against the fp64 oracle: the
+    LDS-FFT Poisson path at its production size, every multi-workgroup seam of the stencil
+    tiles and the column pass. fp32 tolerance as above."""
+    W = H = 2048
+    m = model(W, H, 2, False, dt=0.05, beta=1e-3, nu=0.01)
+    z0 = bo.rossby_mode(W, H, 1.0, 1.0, 5, 3, amp=1e-2) + bo.rossby_mode(W, H, 1.0, 1.0, 2, 7, amp=5e-3)
+    z0 = z0 + 1e-3 * smooth_field(W, H, seed=11)
+    m.set_vorticity(z0)
+    m.run(2)
+    want = bo.run(z0.astype(np.float32).astype(np.float64), 2, 0.05, 1.0, 1.0, 1e-3, 0.01, 2)
+    assert rel(m.get_vorticity_field(), want) < 1e-4

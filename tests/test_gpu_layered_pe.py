@@ -133,3 +133,25 @@ def test_errors():
     c.grid_width, c.grid_height, c.num_levels = 2, 16, 4
     with pytest.raises(ValueError):
         ws.LayeredPrimitiveEquationsModel(c)
+
+
+def test_bench_size_c4p_vs_oracle():
+    """The bench workload itself (config c4p: 1024^2 x 32 layers fp32 RK4, dx 1 km, dt 5 s,
+    f 1e-4, g' 0.02 -- bench.py bench_lpe's initial state) for one step against the float32
+    oracle: 8 x 256 tiles, 4 chunks of levels, the production launch. One step keeps the NumPy
+    oracle to ~20 s."""
+    W = H = 1024
+    L = 32
+    m = model(W, H, L, 2, False, dx=1000.0, dy=1000.0, dt=5.0, f=1e-4, gp=0.02)
+    u, v, h = lp.rest_state(L, H, W, [40.0 + 2.0 * k for k in range(L)])
+    x = np.arange(W)[None, :]
+    y = np.arange(H)[:, None]
+    for k in range(L):
+        h[k] += 0.5 * np.cos(2 * np.pi * (3 * x / W + 2 * y / H) + 0.1 * k)
+        u[k] += 0.01 * np.sin(2 * np.pi * (x / W + 0.05 * k))
+    m.set_state(u, v, h)
+    m.run(1)
+    want = lp.run((u, v, h), 1, 5.0, 1000.0, 1000.0, G, 0.02, 1e-4, 2, dtype=np.float32)
+    for got, w in zip(m.get_state(), want):
+        assert rel(got, w.astype(np.float64)) < 1e-5
+
