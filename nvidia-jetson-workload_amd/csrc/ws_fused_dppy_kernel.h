@@ -75,6 +75,13 @@ __device__ __forceinline__ V3<T> dpp_right(const V3<T>& m) { return V3<T>{from_r
 // of the stage before, which that body writes to a per-wave LDS row (double-buffered by body
 // parity: three ds_write + six ds_read per stage and body). LDS bandwidth and capacity bound
 // how many stages can move (measured).
+// LDS-DMA prefetch distance in groups of kG rows; 0 = by precision (see kPF). Round 1 (one
+// step per launch, exact fp64): 2 or 3 groups measured -3 / -8 %; round 2 (two steps per
+// launch, fast fp64: bodies twice as long, so one group gave the DMA ~1000 cycles): 2 groups
+// +9 %, 3 groups +0 %.
+#ifndef WS_DPPY_PF
+#define WS_DPPY_PF 0
+#endif
 #ifndef WS_DPPY_LDSX
 #define WS_DPPY_LDSX 0x1
 #endif
@@ -95,7 +102,10 @@ struct StepRings {
 template <typename T, int NST, int NSTEP, int MODE>
 __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     constexpr int kG = 16 / (int)sizeof(T);                // rows per DMA instruction
-    constexpr int kD = kG;                                  // DMA rows in flight (one group ahead)
+    // DMA rows in flight: WS_DPPY_PF groups ahead (0 = by precision: fp64 two groups = 4
+    // rows, fp32 one group = 4 rows; C2 two-step fp64: 0.1272 -> 0.1162 ms/step at two)
+    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : (sizeof(T) == 8 ? 2 : 1);
+    constexpr int kD = kG * kPF;
     constexpr int kNR = (kD + kG + 2 + kG - 1) / kG * kG;   // ring: rows R-2 .. R+kD+kG-1, whole groups
     constexpr int kU = kNR;                                 // march unroll: ring slot == phase
     constexpr int kNS = NST * NSTEP;                        // stages per launch (the cone depth)
