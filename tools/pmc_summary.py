@@ -15,7 +15,7 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
             key = (row.get("Dispatch_Id"), row.get("Counter_Name"))
             vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in sorted(vals.items(), key=lambda kv: -len(kv[1])):
-    short = k.split("(")[0][-90:]
+    short = k.replace("(anonymous namespace)::", "").split("(")[0][-90:]
     print(short)
     for c, v in sorted(cs.items()):
         print(f"    {c:24s} mean/dispatch {sum(v) / len(v):16.1f}  (n={len(v)})")
