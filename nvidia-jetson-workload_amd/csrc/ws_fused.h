@@ -84,17 +84,15 @@ __host__ __device__ inline void fused_rows(const FusedArgs<T>& a, int i, int& y0
 template <typename T>
 hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 // "dppy": independent 64-lane waves, one column per lane, horizontal neighbours by DPP lane
-// shifts, y rows staged by LDS-DMA and read from LDS in place.
-constexpr int kDppCols = 64;
-// nsteps = time steps per launch (1, or 2: temporal blocking, see ws_fused_dppy.hip)
+// shifts, y rows staged by LDS-DMA and read from LDS in place. "x2y": the same kernel with an
+// adjacent column pair per lane (128-column strips). variant = kFusedDppLdsY or kFusedX2Y;
+// nsteps = time steps per launch (1, or 2: temporal blocking, see ws_fused_dppy_kernel.h)
 template <typename T>
-hipError_t launch_fused_step_dppy(int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
-// one translation unit per (T, steps per launch): the kernel instantiations
-template <typename T, int NSTEP>
+hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g,
+                                  hipStream_t s);
+// one translation unit per (T, steps per launch, columns per lane): the kernel instantiations
+template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs);
-// "x2y": as dppy with an adjacent column pair per lane (128-column strips).
-template <typename T>
-hipError_t launch_fused_step_x2y(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone,
 // rounded up to whole 16-byte DMA chunks for the LDS-DMA variants: a strip's chunks then

@@ -1,5 +1,5 @@
-// Device helpers shared by the fused step kernels (ws_fused.hip, ws_fused_dppy.hip,
-// ws_fused_x2y.hip): buffer-descriptor memory access, DPP lane shifts, and the SWE tendency
+// Device helpers shared by the fused step kernels (ws_fused.hip, ws_fused_dppy_kernel.h):
+// buffer-descriptor memory access, DPP lane shifts, and the SWE tendency
 // written once for scalar and 2-wide (ext_vector) cell values, per spacing / numerics mode.
 #pragma once
 

@@ -1,19 +1,21 @@
-// Host launcher of the dppy fused step kernel (kernel: ws_fused_dppy_kernel.h; its
-// instantiations: ws_fused_dppy_{f32,f64}_{1,2}.hip).
+// Host launcher of the dppy / x2y fused step kernel (kernel: ws_fused_dppy_kernel.h; its
+// instantiations: ws_fused_dppy{,2}_{f32,f64}_{1,2}.hip).
 #include "ws_fused.h"
 
 namespace ws {
 
-constexpr int kDppyWave = 64;
-
 template <typename T>
-hipError_t launch_fused_step_dppy(int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g, hipStream_t s) {
+hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g,
+                                  hipStream_t s) {
     const int out_w = a.out_w;
+    if (variant != kFusedDppLdsY && variant != kFusedX2Y) return hipErrorInvalidValue;
     if (nsteps != 1 && nsteps != 2) return hipErrorInvalidValue;
     const int ns = nstages * nsteps;  // the launch's cone depth
-    if (out_w < 1 || out_w > kDppyWave - 2 * fused_margin(kFusedDppLdsY, ns, (int)sizeof(T)))
+    if (out_w < 1 || out_w > fused_strip_cols(variant) - 2 * fused_margin(variant, ns, (int)sizeof(T)))
         return hipErrorInvalidValue;
     if (out_w % (16 / (int)sizeof(T)) != 0) return hipErrorInvalidValue;  // chunk-aligned strips
+    // column pairs are stored whole: an odd width's last pair ends in the row padding
+    if (variant == kFusedX2Y && (g.pitch % 2 != 0 || g.pitch < g.W + (g.W % 2))) return hipErrorInvalidValue;
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (nsegs <= 0) return hipSuccess;
@@ -23,11 +25,14 @@ hipError_t launch_fused_step_dppy(int nstages, int nsteps, const FusedArgs<T>& a
     // dropped-store voffset is 2^31
     const int64_t span = (int64_t)(a.seg_rows + 2 * ns + 48) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
-    return nsteps == 1 ? launch_dppy_tu<T, 1>(nstages, a, g, s, nstrips, nsegs)
-                       : launch_dppy_tu<T, 2>(nstages, a, g, s, nstrips, nsegs);
+    if (variant == kFusedX2Y)
+        return nsteps == 1 ? launch_dppy_tu<T, 1, 2>(nstages, a, g, s, nstrips, nsegs)
+                           : launch_dppy_tu<T, 2, 2>(nstages, a, g, s, nstrips, nsegs);
+    return nsteps == 1 ? launch_dppy_tu<T, 1, 1>(nstages, a, g, s, nstrips, nsegs)
+                       : launch_dppy_tu<T, 2, 1>(nstages, a, g, s, nstrips, nsegs);
 }
 
-template hipError_t launch_fused_step_dppy<float>(int, int, const FusedArgs<float>&, const Geom&, hipStream_t);
-template hipError_t launch_fused_step_dppy<double>(int, int, const FusedArgs<double>&, const Geom&, hipStream_t);
+template hipError_t launch_fused_step_dppy<float>(int, int, int, const FusedArgs<float>&, const Geom&, hipStream_t);
+template hipError_t launch_fused_step_dppy<double>(int, int, int, const FusedArgs<double>&, const Geom&, hipStream_t);
 
 }  // namespace ws

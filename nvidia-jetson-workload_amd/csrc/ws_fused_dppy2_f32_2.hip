@@ -1,4 +1,4 @@
-// fused_dppy_kernel instantiations for float, 1 time step(s) per launch, one column per lane (variant dppy)
+// fused_dppy_kernel instantiations for float, 2 time step(s) per launch, column pairs per lane (variant x2y)
 // (see ws_fused_dppy_kernel.h)
 #include "ws_fused_dppy_kernel.h"
 
@@ -7,5 +7,5 @@ template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
     return launch_dppy_impl<T, NSTEP, CPL>(nstages, a, g, s, nstrips, nsegs);
 }
-template hipError_t launch_dppy_tu<float, 1, 1>(int, const FusedArgs<float>&, const Geom&, hipStream_t, int, int);
+template hipError_t launch_dppy_tu<float, 2, 2>(int, const FusedArgs<float>&, const Geom&, hipStream_t, int, int);
 }  // namespace ws

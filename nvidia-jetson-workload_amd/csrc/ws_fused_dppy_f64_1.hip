@@ -1,10 +1,11 @@
-// fused_dppy_kernel instantiations for double, 1 time step per launch (see ws_fused_dppy_kernel.h)
+// fused_dppy_kernel instantiations for double, 1 time step(s) per launch, one column per lane (variant dppy)
+// (see ws_fused_dppy_kernel.h)
 #include "ws_fused_dppy_kernel.h"
 
 namespace ws {
-template <typename T, int NSTEP>
+template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
-    return launch_dppy_impl<T, NSTEP>(nstages, a, g, s, nstrips, nsegs);
+    return launch_dppy_impl<T, NSTEP, CPL>(nstages, a, g, s, nstrips, nsegs);
 }
-template hipError_t launch_dppy_tu<double, 1>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
+template hipError_t launch_dppy_tu<double, 1, 1>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
 }  // namespace ws

@@ -2,6 +2,13 @@
 // column strip, horizontal neighbours by DPP lane shifts (wave_shr:1 / wave_shl:1) -- no
 // workgroup barrier -- and the y rows staged by LDS-DMA and read from LDS in place.
 //
+// Lane width CPL: one column per lane (64-column strips, variant "dppy"), or an adjacent
+// column pair per lane (128-column strips, variant "x2y"). With pairs, of a cell's two
+// horizontal neighbours one is the lane's own other column -- half the DPP moves per cell --
+// the strip overlap is 2 * margin of 128 columns instead of 64, and fp32 pairs run as packed
+// fp32 (v_pk_*) instructions. Every operation is element-wise, so both widths give the
+// same bits.
+//
 // Same march as ws_fused.hip (one kernel per time step; y read once, y' written once;
 // stage s = 1..NST computes row R - s while row R arrives; register rings indexed by a
 // compile-time phase), but every wave runs free: nothing synchronises it with any other
@@ -39,34 +46,77 @@ using namespace dev;
 
 constexpr int kWave = 64;
 
+template <typename T>
+using P2 = T __attribute__((ext_vector_type(2)));
+
+// A lane's cells at a global x edge: its (first) column is x = 0 (lo) / x = W - 1 (hi); a
+// pair's second column is x = W - 1 (hi1; it is never x = 0: pairs start on even columns).
+struct XEdge {
+    bool lo, hi, hi1;
+};
+
 // One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
 // XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
 // the neighbour index to the cell itself (weather_simulation.cpp:510-513).
 // l / r: the mid row's left / right neighbours (DPP lane shifts, or LDS reads: see
-// kLdsStages below).
-template <int MODE, bool XCLAMP, bool YCLAMP, typename T>
-__device__ __forceinline__ V3<T> stage_tend_lr(bool xlo, bool xhi, int j, const Geom& g, const V3<T>& up,
-                                               const V3<T>& mid, const V3<T>& down, V3<T> l, V3<T> r,
-                                               const Spacing<T>& sp, T grav, T cor) {
+// kLdsStages below). VT = T, or P2<T> for a column pair (element-wise).
+template <int MODE, bool XCLAMP, bool YCLAMP, typename VT, typename T>
+__device__ __forceinline__ V3<VT> stage_tend_lr(const XEdge& e, int j, const Geom& g, const V3<VT>& up,
+                                                const V3<VT>& mid, const V3<VT>& down, V3<VT> l, V3<VT> r,
+                                                const Spacing<T>& sp, T grav, T cor) {
     if constexpr (XCLAMP) {
-        l = V3<T>{xlo ? mid.u : l.u, xlo ? mid.v : l.v, xlo ? mid.h : l.h};
-        r = V3<T>{xhi ? mid.u : r.u, xhi ? mid.v : r.v, xhi ? mid.h : r.h};
+        if constexpr (std::is_same_v<VT, T>) {
+            l = V3<VT>{e.lo ? mid.u : l.u, e.lo ? mid.v : l.v, e.lo ? mid.h : l.h};
+            r = V3<VT>{e.hi ? mid.u : r.u, e.hi ? mid.v : r.v, e.hi ? mid.h : r.h};
+        } else {
+            // a pair's inner neighbours are its own columns; only the outer ones clamp
+            if (e.lo) { l.u.x = mid.u.x; l.v.x = mid.v.x; l.h.x = mid.h.x; }
+            if (e.hi) { r.u.x = mid.u.x; r.v.x = mid.v.x; r.h.x = mid.h.x; }
+            if (e.hi1) { r.u.y = mid.u.y; r.v.y = mid.v.y; r.h.y = mid.h.y; }
+        }
     }
     if constexpr (YCLAMP) {
         const bool ytop = (j == 0) && g.top_clamp;
         const bool ybot = (j == g.H - 1) && g.bot_clamp;
-        const V3<T> t{ytop ? mid.u : up.u, ytop ? mid.v : up.v, ytop ? mid.h : up.h};
-        const V3<T> b{ybot ? mid.u : down.u, ybot ? mid.v : down.v, ybot ? mid.h : down.h};
+        const V3<VT> t = ytop ? mid : up;
+        const V3<VT> b = ybot ? mid : down;
         return tend<MODE>(mid, l, r, t, b, sp, grav, cor);
     } else {
         return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
     }
 }
 
+// left / right neighbours by DPP lane shifts: one column per lane -- the neighbouring
+// lanes' values; a column pair (x, y) -- (left lane's y, own x) and (own y, right lane's x)
 template <typename T>
-__device__ __forceinline__ V3<T> dpp_left(const V3<T>& m) { return V3<T>{from_left(m.u), from_left(m.v), from_left(m.h)}; }
+__device__ __forceinline__ void dpp_lr(const T& m, T& l, T& r) {
+    l = from_left(m);
+    r = from_right(m);
+}
 template <typename T>
-__device__ __forceinline__ V3<T> dpp_right(const V3<T>& m) { return V3<T>{from_right(m.u), from_right(m.v), from_right(m.h)}; }
+__device__ __forceinline__ void dpp_lr(const P2<T>& m, P2<T>& l, P2<T>& r) {
+    l = P2<T>{from_left(m.y), m.x};
+    r = P2<T>{m.y, from_right(m.x)};
+}
+template <typename VT>
+__device__ __forceinline__ void dpp_lr3(const V3<VT>& m, V3<VT>& l, V3<VT>& r) {
+    dpp_lr(m.u, l.u, r.u);
+    dpp_lr(m.v, l.v, r.v);
+    dpp_lr(m.h, l.h, r.h);
+}
+// the same from an LDS row of the values (row[lane] = this lane's): lanes 0 / 63 read past
+// the row -- margin lanes only (the previous / next row, or outside the array: LDS returns 0)
+template <typename T>
+__device__ __forceinline__ void lds_lr(const T* row, int lane, const T& m, T& l, T& r) {
+    l = row[lane - 1];
+    r = row[lane + 1];
+}
+template <typename T>
+__device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& m, P2<T>& l, P2<T>& r) {
+    const T* e = reinterpret_cast<const T*>(row);
+    l = P2<T>{e[2 * lane - 1], m.x};
+    r = P2<T>{m.y, e[2 * lane + 2]};
+}
 
 // Stages of the launch's cone (bit gs - 1 for stage gs = q NST + s) that take their
 // horizontal neighbours from LDS instead of DPP lane shifts: an fp64 neighbour is two 32-bit
@@ -91,22 +141,26 @@ __device__ __forceinline__ V3<T> dpp_right(const V3<T>& m) { return V3<T>{from_r
 constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
 
 // Per time step of a launch: the march's register rings (parity-indexed by row)
-template <typename T>
+template <typename VT>
 struct StepRings {
-    V3<T> Y[2];                  // Y[r % 2] = the step's input row r, r <= R-3
-    V3<T> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
-    V3<T> K2[2], K3[2];          // RK4 stage-2 tendency / stage-3 keep (rk4_keep3) at row r
-    V3<T> O[2];                  // the step's last output rows (the next step's input), NSTEP > 1
+    V3<VT> Y[2];                  // Y[r % 2] = the step's input row r, r <= R-3
+    V3<VT> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
+    V3<VT> K2[2], K3[2];          // RK4 stage-2 tendency / stage-3 keep (rk4_keep3) at row r
+    V3<VT> O[2];                  // the step's last output rows (the next step's input), NSTEP > 1
 };
 
-template <typename T, int NST, int NSTEP, int MODE>
+template <typename T, int NST, int NSTEP, int MODE, int CPL>
 __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
-    constexpr int kG = 16 / (int)sizeof(T);                // rows per DMA instruction
-    // DMA rows in flight: WS_DPPY_PF groups ahead (0 = by precision: fp64 two groups = 4
-    // rows, fp32 one group = 4 rows; C2 two-step fp64: 0.1272 -> 0.1162 ms/step at two)
-    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : (sizeof(T) == 8 ? 2 : 1);
+    static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
+    using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
+    constexpr int kG = 16 / (int)sizeof(VT);               // rows per DMA instruction
+    // DMA rows in flight: WS_DPPY_PF groups ahead (0 = 4 rows of 64 columns, 2 rows of
+    // column pairs -- about the same time ahead, a pair body being twice as long; C2
+    // two-step fp64: 0.1272 -> 0.1162 ms/step at 4 rows against 2)
+    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : ((4 / CPL) / kG > 1 ? (4 / CPL) / kG : 1);
     constexpr int kD = kG * kPF;
-    constexpr int kNR = (kD + kG + 2 + kG - 1) / kG * kG;   // ring: rows R-2 .. R+kD+kG-1, whole groups
+    constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
+    constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1
     constexpr int kU = kNR;                                 // march unroll: ring slot == phase
     constexpr int kNS = NST * NSTEP;                        // stages per launch (the cone depth)
     // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on
@@ -135,11 +189,14 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     const int lane = (int)threadIdx.x;
     // left margin: the cone (kNS) rounded up to whole 16-byte chunks, so a strip's DMA chunks
     // never straddle column 0 (a partly negative chunk is dropped whole by the range check)
-    constexpr int kM = (kNS + kG - 1) / kG * kG;
+    constexpr int kC = 16 / (int)sizeof(T);  // columns per chunk
+    constexpr int kM = (kNS + kC - 1) / kC * kC;
     const int out_w = a.out_w;
-    const int x = strip * out_w - kM + lane;  // this lane's global column
-    const bool xout = x >= 0 && x < g.W && lane >= kM && lane < kM + out_w;
-    const bool xlo = x == 0, xhi = x == g.W - 1;
+    const int x = strip * out_w - kM + CPL * lane;  // this lane's (first) global column
+    // a pair is stored whole: its second column is x + 1 < W, or row padding (x < W <= pitch,
+    // both even), whose content is unspecified
+    const bool xout = x >= 0 && x < g.W && CPL * lane >= kM && CPL * lane < kM + out_w;
+    const XEdge xe{x == 0, x == g.W - 1, CPL == 2 && x + 1 == g.W - 1};
 
     const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
     const int row_hi = g.bot_clamp ? g.H : g.H + g.halo;
@@ -165,18 +222,18 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     // Stores are issued for every row, unconditionally: rows outside [y0, y1) are dropped by
     // the range check through the voffset (a branch around them makes the compiler's vmcnt
     // bookkeeping merge both paths and drain the prefetch at every row).
-    auto store_row = [&](int j, const V3<T>& o) {
+    auto store_row = [&](int j, const V3<VT>& o) {
         const bool row_ok = j >= y0 && j < y1;
         const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
         const uint32_t vo = row_ok ? soff : kDropped;
-        buf_store_nt<T>(o.u, wu, vo, so);
-        buf_store_nt<T>(o.v, wv, vo, so);
-        buf_store_nt<T>(o.h, wh, vo, so);
+        buf_store_nt<VT>(o.u, wu, vo, so);
+        buf_store_nt<VT>(o.v, wv, vo, so);
+        buf_store_nt<VT>(o.h, wh, vo, so);
     };
 
     // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG
-    // consecutive slots (64 lanes x 16 B = kG rows of 64 columns)
-    __shared__ __attribute__((aligned(16))) T ring[3][kNR][kWave];
+    // consecutive slots (64 lanes x 16 B = kG rows of the strip)
+    __shared__ __attribute__((aligned(16))) VT ring[3][kNR][kWave];
     const int dk = lane / (kWave / kG);  // row of the group this lane fetches
     const int dcol = (strip * out_w - kM) * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // 16-B aligned
     auto dma = [&](int q, int slot) {  // rows q .. q + kG - 1 into slots slot .. slot + kG - 1
@@ -189,18 +246,10 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
         lds_dma16(rv, &ring[1][slot][0], vo);
         lds_dma16(rh, &ring[2][slot][0], vo);
     };
-    auto read_row = [&](int slot) -> V3<T> { return V3<T>{ring[0][slot][lane], ring[1][slot][lane], ring[2][slot][lane]}; };
-    // a ring row's neighbours: lanes 0 / 63 read past the row (the previous / next slot, or
-    // outside the array: LDS returns 0) -- margin lanes only
-    auto ring_left = [&](int slot) -> V3<T> {
-        return V3<T>{ring[0][slot][lane - 1], ring[1][slot][lane - 1], ring[2][slot][lane - 1]};
-    };
-    auto ring_right = [&](int slot) -> V3<T> {
-        return V3<T>{ring[0][slot][lane + 1], ring[1][slot][lane + 1], ring[2][slot][lane + 1]};
-    };
+    auto read_row = [&](int slot) -> V3<VT> { return V3<VT>{ring[0][slot][lane], ring[1][slot][lane], ring[2][slot][lane]}; };
     // per-wave LDS rows of the LDS-neighbour stages: xrow[parity][slot][field][lane]
-    __shared__ T xrow[2][kNX > 0 ? kNX : 1][3][kWave];
-    auto xput = [&](auto Pc, auto GSc, const V3<T>& v) {
+    __shared__ VT xrow[2][kNX > 0 ? kNX : 1][3][kWave];
+    auto xput = [&](auto Pc, auto GSc, const V3<VT>& v) {
         constexpr int P = decltype(Pc)::value, gs = decltype(GSc)::value;
         if constexpr (gs > 1 && ldsx(gs)) {
             auto& b = xrow[P % 2][xslot(gs)];
@@ -210,23 +259,27 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
         }
     };
     // neighbours of stage gs's mid row `mid` (its ring slot `rs` for stage 1)
-    auto nbrs = [&](auto Pc, auto GSc, const V3<T>& mid, int rs, V3<T>& l, V3<T>& r) {
+    auto nbrs = [&](auto Pc, auto GSc, const V3<VT>& mid, int rs, V3<VT>& l, V3<VT>& r) {
         constexpr int P = decltype(Pc)::value, gs = decltype(GSc)::value;
         if constexpr (!ldsx(gs)) {
-            l = dpp_left(mid);
-            r = dpp_right(mid);
-        } else if constexpr (gs == 1) {
-            l = ring_left(rs);
-            r = ring_right(rs);
+            dpp_lr3(mid, l, r);
         } else {
-            auto& b = xrow[(P + 1) % 2][xslot(gs)];
-            l = V3<T>{b[0][lane - 1], b[1][lane - 1], b[2][lane - 1]};
-            r = V3<T>{b[0][lane + 1], b[1][lane + 1], b[2][lane + 1]};
+            // stage 1: the mid row's ring slot; later stages: the previous body's LDS row
+            if constexpr (gs == 1) {
+                lds_lr(ring[0][rs], lane, mid.u, l.u, r.u);
+                lds_lr(ring[1][rs], lane, mid.v, l.v, r.v);
+                lds_lr(ring[2][rs], lane, mid.h, l.h, r.h);
+            } else {
+                auto& b = xrow[(P + 1) % 2][xslot(gs)];
+                lds_lr(b[0], lane, mid.u, l.u, r.u);
+                lds_lr(b[1], lane, mid.v, l.v, r.v);
+                lds_lr(b[2], lane, mid.h, l.h, r.h);
+            }
         }
     };
 
-    const V3<T> Z{T(0), T(0), T(0)};
-    StepRings<T> st[NSTEP];
+    const V3<VT> Z{VT{}, VT{}, VT{}};
+    StepRings<VT> st[NSTEP];
 #pragma unroll
     for (int q = 0; q < NSTEP; ++q)
 #pragma unroll
@@ -241,8 +294,8 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     // needs it (warm-up: the first bodies of a segment skip stages outside the segment's
     // cone; whatever a body computes beyond the cone only ever reaches rows that are not
     // stored). Ring slots are indexed by the parity of the body phase P.
-    auto step = [&](auto Qc, auto Pc, auto Xc, auto Yc, auto ONc, StepRings<T>& S, const V3<T>& i0,
-                    const V3<T>& i1, const V3<T>& i2, int Rq, V3<T>& out) {
+    auto step = [&](auto Qc, auto Pc, auto Xc, auto Yc, auto ONc, StepRings<VT>& S, const V3<VT>& i0,
+                    const V3<VT>& i1, const V3<VT>& i2, int Rq, V3<VT>& out) {
         constexpr int q = decltype(Qc)::value;
         constexpr int P = decltype(Pc)::value;
         constexpr bool XC = decltype(Xc)::value;
@@ -263,34 +316,34 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
             // a temp / next grid (the config's spacing sp2; the host launches two steps at once
             // only when sp1 == sp2)
             const Spacing<T>& sp_in = q == 0 ? a.sp1 : a.sp2;
-            V3<T> l, r;
+            V3<VT> l, r;
             nbrs(Pc, gsc(S1c{}), i1, rs1, l, r);
-            const V3<T> k1 =
-                stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 1, g, i2, i1, i0, l, r, sp_in, a.gravity, a.coriolis_f);
+            const V3<VT> k1 =
+                stage_tend_lr<MODE, XC, YC>(xe, Rq - 1, g, i2, i1, i0, l, r, sp_in, a.gravity, a.coriolis_f);
             if constexpr (NST == 1) {
                 out = axpy<MODE>(i1, a.c_dt, k1);  // Euler: y + dt k
             } else {
-                const V3<T> s1 = axpy<MODE>(i1, a.c_half, k1);  // y + (0.5f dt) k
+                const V3<VT> s1 = axpy<MODE>(i1, a.c_half, k1);  // y + (0.5f dt) k
                 xput(Pc, gsc(S2c{}), s1);
                 if constexpr (on(2)) {
                     nbrs(Pc, gsc(S2c{}), S.S1[r2(-2)], 0, l, r);
-                    const V3<T> k2 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
+                    const V3<VT> k2 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
                                                                  l, r, a.sp2, a.gravity, a.coriolis_f);
                     if constexpr (NST == 2) {
                         out = axpy<MODE>(i2, a.c_dt, k2);  // RK2: y + dt k2
                     } else {
-                        const V3<T> s2 = axpy<MODE>(i2, a.c_half, k2);
+                        const V3<VT> s2 = axpy<MODE>(i2, a.c_half, k2);
                         xput(Pc, gsc(S3c{}), s2);
                         if constexpr (on(3)) {
                             nbrs(Pc, gsc(S3c{}), S.S2[r2(-3)], 0, l, r);
-                            const V3<T> k3 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 3, g, S.S2[r2(-4)],
+                            const V3<VT> k3 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 3, g, S.S2[r2(-4)],
                                                                          S.S2[r2(-3)], s2, l, r, a.sp2, a.gravity,
                                                                          a.coriolis_f);
-                            const V3<T> s3 = axpy<MODE>(S.Y[r2(-3)], a.c_dt, k3);
+                            const V3<VT> s3 = axpy<MODE>(S.Y[r2(-3)], a.c_dt, k3);
                             xput(Pc, gsc(S4c{}), s3);
                             if constexpr (on(4)) {
                                 nbrs(Pc, gsc(S4c{}), S.S3[r2(-4)], 0, l, r);
-                                const V3<T> k4 = stage_tend_lr<MODE, XC, YC>(xlo, xhi, Rq - 4, g, S.S3[r2(-5)],
+                                const V3<VT> k4 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 4, g, S.S3[r2(-5)],
                                                                              S.S3[r2(-4)], s3, l, r, a.sp2, a.gravity,
                                                                              a.coriolis_f);
                                 // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
@@ -325,20 +378,20 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
             dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies
             __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));  // rows R .. R+kG-1 have landed
         }
-        const V3<T> yR0 = read_row(sl(0)), yR1 = read_row(sl(-1)), yR2 = read_row(sl(-2));
+        const V3<VT> yR0 = read_row(sl(0)), yR1 = read_row(sl(-1)), yR2 = read_row(sl(-2));
         // keep the row's DMA at the head of the body: the scheduler would otherwise sink it
         // below the stencil math, shortening the prefetch distance
         __builtin_amdgcn_sched_barrier(0);
-        V3<T> o0 = Z;
+        V3<VT> o0 = Z;
         step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o0);
         if constexpr (NSTEP == 1) {
             if constexpr (On{}(NST)) store_row(R - NST, o0);
             else store_row(y0 - 1, Z);
         } else {
             // step 2's input rows R-NST (just computed), R-NST-1, R-NST-2 (step 1's ring)
-            const V3<T> i1 = st[0].O[r2(-NST - 1)], i2 = st[0].O[r2(-NST - 2)];
+            const V3<VT> i1 = st[0].O[r2(-NST - 1)], i2 = st[0].O[r2(-NST - 2)];
             if constexpr (On{}(NST)) st[0].O[r2(-NST)] = o0;  // the slot of row R-NST-2, read above
-            V3<T> o1 = Z;
+            V3<VT> o1 = Z;
             step(std::integral_constant<int, 1>{}, Pc, Xc, Yc, On{}, st[1], o0, i1, i2, R - NST, o1);
             if constexpr (On{}(2 * NST)) store_row(R - 2 * NST, o1);
             else store_row(y0 - 1, Z);
@@ -383,12 +436,13 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
 
 }  // namespace
 
-// Launch fused_dppy_kernel<T, nstages, NSTEP, mode> (one translation unit per (T, NSTEP):
-// ws_fused_dppy_<t><n>.hip, compiled in parallel).
-template <typename T, int NSTEP>
+// Launch fused_dppy_kernel<T, nstages, NSTEP, mode, CPL> (one translation unit per (T,
+// NSTEP, CPL): ws_fused_dppy{,2}_<t>_<n>.hip, compiled in parallel).
+template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
     const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(kWave);
-#define WS_DPPY_GO(N, M) hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M>), grid, block, 0, s, a, g, nstrips, nsegs)
+#define WS_DPPY_GO(N, M) \
+    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL>), grid, block, 0, s, a, g, nstrips, nsegs)
 #define WS_DPPY_G1(M) WS_DPPY_GO(1, M)
 #define WS_DPPY_G2(M) WS_DPPY_GO(2, M)
 #define WS_DPPY_G4(M) WS_DPPY_GO(4, M)

@@ -274,7 +274,7 @@ struct ws_sim {
     int out_w(int cone) const { return ws::fused_out_w(kernel, cone, (int)elem_size(dtype), align); }
     int64_t strips(int cone) const { return (slot[0]->W + out_w(cone) - 1) / out_w(cone); }
     // steps per launch the tuned configuration asks for (1 unless dppy with tb = 2)
-    int launch_tb() const { return kernel == kKernDppLdsY ? tb : 1; }
+    int launch_tb() const { return kernel == kKernLds ? 1 : tb; }
     // segment rows giving about want_blocks workgroups (at least min_rows rows; the march
     // length rows + 2 NST a multiple of the unroll)
     int32_t seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const {
@@ -391,12 +391,9 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
     const ws::Geom g = c->geom();
-    if (nsteps > 1 && s->kernel != kKernDppLdsY) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy");
-    switch (s->kernel) {
-        case kKernX2Y: WS_HIP_CHECK(ws::launch_fused_step_x2y<T>(nst, a, g, st)); break;
-        case kKernDppLdsY: WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(nst, nsteps, a, g, st)); break;
-        default: WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st)); break;
-    }
+    if (nsteps > 1 && s->kernel == kKernLds) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy or x2y");
+    if (s->kernel == kKernLds) WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st));
+    else WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(s->kernel, nst, nsteps, a, g, st));
     ++s->last_launches;
 }
 
@@ -553,8 +550,8 @@ void autotune_time(ws_sim* s) {
     const bool tb2_ok = s->block >= 2 || s->nranks == 1;
     for (int k : {kKernDppLdsY, kKernX2Y, kKernLds})
       for (int tb : {1, 2}) {
-        if (tb == 2 && (k != kKernDppLdsY || !tb2_ok)) continue;
-        if (s->tb_fixed && k == kKernDppLdsY && tb != fixed_tb) continue;
+        if (tb == 2 && (k == kKernLds || !tb2_ok)) continue;
+        if (s->tb_fixed && k != kKernLds && tb != fixed_tb) continue;
         s->tb = tb;
         const int cone = nst * tb;
         for (bool al : {false, true}) {

@@ -72,10 +72,11 @@ def _fields(grid):
     return {"u": u, "v": v, "h": grid.get_height_field(), "vort": grid.get_vorticity_field()}
 
 
-@pytest.mark.parametrize("ic,tb", [("jet_stream", None), ("random", "1"), ("random", "2")])
-def test_c5_single_gpu_matches_reference_bands(ic, tb, monkeypatch):
+@pytest.mark.parametrize("ic,kernel,tb", [("jet_stream", None, None), ("random", "dppy", "1"), ("random", "dppy", "2"),
+                                          ("random", "x2y", "2")])
+def test_c5_single_gpu_matches_reference_bands(ic, kernel, tb, monkeypatch):
     if tb:
-        monkeypatch.setenv("WS_KERNEL", "dppy")
+        monkeypatch.setenv("WS_KERNEL", kernel)
         monkeypatch.setenv("WS_TB", tb)
     fx = _fixtures()
     sim = ws.WeatherSimulation(_cfg(fx))

@@ -58,11 +58,12 @@ def load(sim, s0):
 
 # (WS_FUSED, WS_KERNEL, WS_TB): every fused variant, dppy also with two steps per launch
 # (temporal blocking: run(n) advances pairs of steps per launch), and the per-stage kernels
-KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "lds", "1"), ("0", "x2y", "1")]
-KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_lds", "stage_kernels"]
+KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "x2y", "2"), ("1", "lds", "1"),
+           ("0", "x2y", "1")]
+KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_x2y_tb2", "fused_lds", "stage_kernels"]
 # (kernel, steps per launch) of the fused variants
-FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("lds", "1")]
-FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "lds"]
+FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("lds", "1")]
+FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "x2y_tb2", "lds"]
 
 
 @pytest.mark.parametrize("fused,kernel,tb", KERNELS, ids=KERNEL_IDS)
@@ -381,6 +382,7 @@ def test_fused_non_pow2_spacing_vs_oracle():
 
 @pytest.mark.parametrize("kernel,seg_rows,tb", [("dppy", "6", "1"), ("dppy", "0", "1"), ("dppy", "6", "2"),
                                                  ("dppy", "0", "2"), ("x2y", "6", "1"), ("x2y", "0", "1"),
+                                                 ("x2y", "6", "2"),
                                                  ("lds", "6", "1"), ("lds", "0", "1")])
 @pytest.mark.parametrize("nslabs", [2, 3, 5])
 @pytest.mark.parametrize("method", [0, 1, 2])

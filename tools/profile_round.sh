@@ -13,7 +13,7 @@ rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$
 read KERN KNAME SEG ALIGN TB < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
 k={'fused_dppy':'dppy','fused_x2y':'x2y','fused_lds':'lds'}.get(d['kernel'],'dppy')
-n={'dppy':'fused_dppy_kernel','x2y':'fused_x2y_kernel','lds':'fused_step_kernel'}[k]
+n={'dppy':'fused_dppy_kernel','x2y':'fused_dppy_kernel','lds':'fused_step_kernel'}[k]
 tb=d.get('steps_per_launch') or 1
 nst={'euler':1,'rk2':2,'rk4':4}['$METHOD']
 nst=2 if nst==4 and '$CFG' in ('c3','c4') else nst
