@@ -154,10 +154,10 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
     constexpr int kG = 16 / (int)sizeof(VT);               // rows per DMA instruction
-    // DMA rows in flight: WS_DPPY_PF groups ahead (0 = 4 rows of 64 columns, 2 rows of
-    // column pairs -- about the same time ahead, a pair body being twice as long; C2
-    // two-step fp64: 0.1272 -> 0.1162 ms/step at 4 rows against 2)
-    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : ((4 / CPL) / kG > 1 ? (4 / CPL) / kG : 1);
+    // DMA rows in flight: WS_DPPY_PF groups ahead (0 = 4 rows; C2 two-step fp64: 0.1272 ->
+    // 0.1162 ms/step at 4 rows against 2; C3 fp32 pairs: 0.0260 -> 0.0222 at 4 rows
+    // against 2, 0.0256 at 6)
+    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
     constexpr int kD = kG * kPF;
     constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
     constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1
