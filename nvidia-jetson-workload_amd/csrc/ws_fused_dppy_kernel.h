@@ -16,9 +16,9 @@
 // redundancy: a 64-column strip outputs 64 - 2*margin columns.
 //
 // y rows: LDS-DMA (buffer_load_dwordx4 ... lds, 16 bytes per lane: one instruction per
-// field moves kG = 16 / sizeof(T) rows of the strip) into a ring one group ahead; each body
-// reads the three rows stage 1 needs (R-2, R-1, R) straight from the ring, only rows R-3
-// and R-4 (the late stage updates) live in VGPRs -- three waves per SIMD fit (RK4 fp64).
+// field moves kG = 16 / (CPL sizeof(T)) rows of the strip) into a ring kD rows ahead; each
+// body reads the three rows stage 1 needs (R-2, R-1, R) straight from the ring, only rows R-3
+// and R-4 (the late stage updates) live in VGPRs.
 // The compiler does not order LDS reads after LDS-DMA writes, so the kernel waits itself:
 // every body issues exactly 3 stores and every kG-th body 3 DMAs, a fixed count of younger
 // vector-memory ops at each wait (kWaitN).
@@ -113,9 +113,10 @@ __device__ __forceinline__ void lds_lr(const T* row, int lane, const T& m, T& l,
 }
 template <typename T>
 __device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& m, P2<T>& l, P2<T>& r) {
-    const T* e = reinterpret_cast<const T*>(row);
-    l = P2<T>{e[2 * lane - 1], m.x};
-    r = P2<T>{m.y, e[2 * lane + 2]};
+    // whole neighbouring pairs (lane-contiguous reads, no bank conflicts; reading the single
+    // columns 2 lane - 1 / 2 lane + 2 strides the banks by two)
+    l = P2<T>{row[lane - 1].y, m.x};
+    r = P2<T>{m.y, row[lane + 1].x};
 }
 
 // Stages of the launch's cone (bit gs - 1 for stage gs = q NST + s) that take their
@@ -124,7 +125,9 @@ __device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& 
 // ring (two extra ds_read per field); a later stage's mid row is the previous body's output
 // of the stage before, which that body writes to a per-wave LDS row (double-buffered by body
 // parity: three ds_write + six ds_read per stage and body). LDS bandwidth and capacity bound
-// how many stages can move (measured).
+// how many stages can move (measured). Default (-1): stage 1 for one column
+// per lane; none for column pairs, whose DPP moves are already halved (C3 fp32 pairs: 0.0183
+// -> 0.0167 ms/step without the LDS reads, C4 0.145 -> 0.133).
 // LDS-DMA prefetch distance in groups of kG rows; 0 = by precision (see kPF). Round 1 (one
 // step per launch, exact fp64): 2 or 3 groups measured -3 / -8 %; round 2 (two steps per
 // launch, fast fp64: bodies twice as long, so one group gave the DMA ~1000 cycles): 2 groups
@@ -133,7 +136,7 @@ __device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& 
 #define WS_DPPY_PF 0
 #endif
 #ifndef WS_DPPY_LDSX
-#define WS_DPPY_LDSX 0x1
+#define WS_DPPY_LDSX -1
 #endif
 
 // s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
     // drop below the threshold while the group is still in flight (seen as stale rows at
     // 4096^2). Loads complete in order.
     constexpr int kWaitN = 3 * (kD / kG);
-    constexpr unsigned kLdsX = (unsigned)(WS_DPPY_LDSX) & ((1u << kNS) - 1u);
+    constexpr unsigned kLdsX = (WS_DPPY_LDSX >= 0 ? (unsigned)(WS_DPPY_LDSX) : CPL == 1 ? 0x1u : 0x0u) & ((1u << kNS) - 1u);
     constexpr auto ldsx = [](int gs) { return ((kLdsX >> (gs - 1)) & 1u) != 0; };
     // LDS row slots of the stages (other than stage 1) that read neighbours from LDS
     constexpr auto xslot = [](int gs) { return __builtin_popcount(kLdsX & ((1u << (gs - 1)) - 1u) & ~1u); };
