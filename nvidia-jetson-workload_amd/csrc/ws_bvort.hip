@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <hipfft/hipfft.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(256) void bv_rowfft_fwd(const T* z, Cx<T>* spec, co
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
     Cx<T>* twl = a + padded(W);  // twiddles staged in LDS: every pass reads them
-    const int nk = W / 2 + 1;
+    const int nk = W / 2;        // spectrum columns: k = 1 .. W/2-1, plus the packed real bins in column 0
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
     for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
     for (int i = threadIdx.x; i < W; i += blockDim.x) a[P(bitrev(i, logw))] = Cx<T>{z[r0 * W + i], z[r1 * W + i]};
@@ -254,20 +255,34 @@ __global__ __launch_bounds__(256) void bv_rowfft_fwd(const T* z, Cx<T>* spec, co
     fft_dit<T, false>(a, twl, W, logw, 1);
     const T h = T(0.5);
     for (int k = threadIdx.x; k < nk; k += blockDim.x) {
-        const Cx<T> zk = a[P(k)], zm = a[P((W - k) & (W - 1))];  // Z(k), Z(W - k)
+        const Cx<T> zk = a[P(k)];
+        if (k == 0) {
+            // the real bins A(0) = Re Z(0), A(W/2) = Re Z(W/2) (B: the imaginary parts) share
+            // column 0 as A(0) + i A(W/2): the column pass transforms both real columns at once
+            const Cx<T> zn = a[P(W / 2)];
+            spec[r0 * nk] = Cx<T>{zk.x, zn.x};
+            spec[r1 * nk] = Cx<T>{zk.y, zn.y};
+            continue;
+        }
+        const Cx<T> zm = a[P(W - k)];  // Z(W - k)
         // A = (Z(k) + conj Z(W-k)) / 2, B = (Z(k) - conj Z(W-k)) / 2i
         spec[r0 * nk + k] = Cx<T>{(zk.x + zm.x) * h, (zk.y - zm.y) * h};
         spec[r1 * nk + k] = Cx<T>{(zk.y + zm.y) * h, (zm.x - zk.x) * h};
     }
 }
 
+// nk = W/2 spectrum columns (column 0 = the packed real bins, see bv_rowfft_fwd), cw per
+// workgroup; the grid is mapped XCD-major (workgroup b runs on XCD b % 8) so the workgroups
+// that share the 128-byte lines of a spectrum row segment share one L2
 template <typename T>
 __global__ __launch_bounds__(1024) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw, const T* ax, const T* ay, int nk,
                                                     int H, int logh, int cw, T norm) {
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
     Cx<T>* twl = a + padded((size_t)cw * H);
-    const int k0 = blockIdx.x * cw;
+    const int nblk = gridDim.x;
+    const int blk = (nblk & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3));
+    const int k0 = blk * cw;
     const int ncol = min(cw, nk - k0);
     for (int i = threadIdx.x; i < H / 2; i += blockDim.x) twl[i] = tw[i];
     for (int i = threadIdx.x; i < H * cw; i += blockDim.x) {
@@ -279,7 +294,21 @@ __global__ __launch_bounds__(1024) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw
     for (int i = threadIdx.x; i < H * ncol; i += blockDim.x) {
         const int c = i / H, l = i - c * H;
         const int k = k0 + c;
-        const T m = (k == 0 && l == 0) ? T(0) : norm / (ax[k] + ay[l]);
+        if (k == 0) {
+            // packed column Z = C0 + i CN (C0, CN: spectra of the real bins' columns, both
+            // Hermitian); scaled separately by s0 = norm / lambda(0, l) (0 at l = 0) and
+            // sN = norm / lambda(W/2, l), recombined: Z'(l) = (s0 + sN)/2 Z(l) + (s0 - sN)/2 conj Z(-l)
+            if (l > H / 2) continue;  // the pair (l, H - l) is done by the thread of l
+            const int n = (H - l) & (H - 1);
+            const T s0 = l == 0 ? T(0) : norm / (ax[0] + ay[l]);
+            const T sN = norm / (ax[nk] + ay[l]);
+            const T p = (s0 + sN) * T(0.5), q = (s0 - sN) * T(0.5);
+            const Cx<T> zl = a[P(l)], zn = a[P(n)];
+            a[P(l)] = Cx<T>{p * zl.x + q * zn.x, p * zl.y - q * zn.y};
+            if (n != l) a[P(n)] = Cx<T>{p * zn.x + q * zl.x, p * zn.y - q * zl.y};
+            continue;
+        }
+        const T m = norm / (ax[k] + ay[l]);
         a[P(i)].x *= m;
         a[P(i)].y *= m;
     }
@@ -296,14 +325,21 @@ __global__ __launch_bounds__(256) void bv_rowfft_inv(const Cx<T>* spec, T* psi, 
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
     Cx<T>* twl = a + padded(W);
-    const int nk = W / 2 + 1;
+    const int nk = W / 2;  // column 0 packs the real bins: A(0) + i A(W/2)
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
     for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
     for (int k = threadIdx.x; k < W; k += blockDim.x) {
-        const bool lo = k < nk;
+        const bool lo = k <= nk;
         const int kk = lo ? k : W - k;
-        Cx<T> A = spec[r0 * nk + kk], B = spec[r1 * nk + kk];
-        if (kk == 0 || kk == W / 2) A.y = B.y = T(0);  // C2R: the real bins' imaginary parts are ignored
+        Cx<T> A, B;
+        if (kk == 0 || kk == nk) {  // C2R: the real bins' imaginary parts are ignored
+            const Cx<T> a0 = spec[r0 * nk], b0 = spec[r1 * nk];
+            A = Cx<T>{kk == 0 ? a0.x : a0.y, T(0)};
+            B = Cx<T>{kk == 0 ? b0.x : b0.y, T(0)};
+        } else {
+            A = spec[r0 * nk + kk];
+            B = spec[r1 * nk + kk];
+        }
         if (!lo) {
             A.y = -A.y;
             B.y = -B.y;
@@ -394,13 +430,15 @@ void upload_eigen(ws_bvort* b) {
 template <typename T>
 void poisson_lds(ws_bvort* b, const void* zin) {
     const size_t cs = 2 * sizeof(T);
-    const int nk = b->W / 2 + 1;
+    const int nk = b->W / 2;  // spectrum columns of the LDS path (real bins packed in column 0)
     Cx<T>* spec = (Cx<T>*)b->spec;
     const size_t row_lds = (padded(b->W) + b->W / 2) * cs, col_lds = (padded((size_t)b->cw * b->H) + b->H / 2) * cs;
     hipLaunchKernelGGL((bv_rowfft_fwd<T>), dim3(b->H / 2), dim3(256), row_lds, b->stream, (const T*)zin, spec,
                        (const Cx<T>*)b->twW, b->W, b->logw);
     hck(hipGetLastError(), "bv_rowfft_fwd");
-    hipLaunchKernelGGL((bv_colsolve<T>), dim3((nk + b->cw - 1) / b->cw), dim3(1024), col_lds,
+    // one radix-8 group per thread and pass
+    const int col_threads = std::min(1024, std::max(64, b->cw * b->H / 8));
+    hipLaunchKernelGGL((bv_colsolve<T>), dim3((nk + b->cw - 1) / b->cw), dim3(col_threads), col_lds,
                        b->stream, spec, (const Cx<T>*)b->twH, (const T*)b->ax, (const T*)b->ay, nk, b->H, b->logh,
                        b->cw, (T)(1.0 / ((double)b->W * b->H)));
     hck(hipGetLastError(), "bv_colsolve");
