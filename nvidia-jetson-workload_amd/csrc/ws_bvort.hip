@@ -54,14 +54,22 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
     __shared__ T Z[kTY + 2][kTX + 2];
     const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
     const int tid = threadIdx.y * kTX + threadIdx.x;
+    // (x0 + lx - 1) lies in [-1, W + kTX], (y0 + ly - 1) in [-1, H + kTY]: one wrap step
+    // covers grids at least a tile (+ halo) wide and tall (a wave-uniform test); narrower
+    // grids reduce fully (an integer division per element: the fill's dominant VALU cost)
+    const bool wide = a.W >= kTX + 2 && a.H >= kTY + 2;
     for (int i = tid; i < (kTY + 2) * (kTX + 2); i += kTX * kBY) {
-        const int ly = i / (kTX + 2), lx = i % (kTX + 2);
-        // (x0 + lx - 1) lies in [-1, W + 64]: one wrap step is not enough past the grid's
-        // end for narrow grids, so reduce fully
-        int gx = (x0 + lx - 1) % a.W;
-        if (gx < 0) gx += a.W;
-        int gy = (y0 + ly - 1) % a.H;
-        if (gy < 0) gy += a.H;
+        const int ly = i / (kTX + 2), lx = i - ly * (kTX + 2);
+        int gx = x0 + lx - 1, gy = y0 + ly - 1;
+        if (wide) {
+            gx = gx < 0 ? gx + a.W : (gx >= a.W ? gx - a.W : gx);
+            gy = gy < 0 ? gy + a.H : (gy >= a.H ? gy - a.H : gy);
+        } else {
+            gx %= a.W;
+            if (gx < 0) gx += a.W;
+            gy %= a.H;
+            if (gy < 0) gy += a.H;
+        }
         const int64_t o = (int64_t)gy * a.W + gx;
         P[ly][lx] = a.psi[o];
         Z[ly][lx] = a.zin[o];
@@ -151,6 +159,14 @@ __host__ __device__ constexpr size_t padded(size_t n) { return n + n / 16 + 1; }
 
 __device__ __forceinline__ int bitrev(int i, int logn) { return (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - logn)); }
 
+// Workgroup barrier ordering LDS traffic only (the FFT passes exchange data through LDS; no
+// global-memory fence needed between them)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Radix-2 stages taken R at a time in registers (one LDS pass and one barrier per R stages):
 // a thread owns the 2^R elements base + j + m h (m < 2^R, j < h) that those stages combine.
 // DIT: stages s .. s+R-1 (h = 2^(s-1)); input bit-reversed, output natural after all passes.
@@ -184,7 +200,7 @@ __device__ __forceinline__ void dit_pass(Cx<T>* a, const Cx<T>* tw, int n, int l
 #pragma unroll
         for (int m = 0; m < M; ++m) a[P(base + m * h)] = x[m];
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // DIF: stages s, s-1, .., s-R+1 (h = 2^(s-R), the smallest half); input natural, output
@@ -220,7 +236,7 @@ __device__ __forceinline__ void dif_pass(Cx<T>* a, const Cx<T>* tw, int n, int l
 #pragma unroll
         for (int m = 0; m < M; ++m) a[P(base + m * h)] = x[m];
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // radix-2 decimation in time over ncol columns of length n (column c at a + c * n), input in
@@ -242,19 +258,27 @@ __device__ void fft_dif(Cx<T>* a, const Cx<T>* tw, int n, int logn, int ncol) {
     else if (s == 1) dif_pass<T, INV, 1>(a, tw, n, logn, s, ncol);
 }
 
+constexpr int kRowThreads = 256;
+constexpr int kColPer = 8;  // column pass: elements per thread, cw H <= 8 kColThreads (one radix-8 group per pass)
 template <typename T>
-__global__ __launch_bounds__(256) void bv_rowfft_fwd(const T* z, Cx<T>* spec, const Cx<T>* tw, int W, int logw) {
+constexpr int kColThreads = sizeof(T) == 8 ? 512 : 1024;
+
+// One pair of rows per workgroup. (Persistent workgroups walking several pairs with the next
+// pair's loads in flight during the FFT measured slower: 16.4-17.1 us against 14.5 at 2048^2
+// fp32 -- the prefetch registers cost a wave per SIMD of occupancy.)
+template <typename T>
+__global__ __launch_bounds__(kRowThreads) void bv_rowfft_fwd(const T* z, Cx<T>* spec, const Cx<T>* tw, int W, int logw) {
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
     Cx<T>* twl = a + padded(W);  // twiddles staged in LDS: every pass reads them
     const int nk = W / 2;        // spectrum columns: k = 1 .. W/2-1, plus the packed real bins in column 0
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
-    for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
-    for (int i = threadIdx.x; i < W; i += blockDim.x) a[P(bitrev(i, logw))] = Cx<T>{z[r0 * W + i], z[r1 * W + i]};
-    __syncthreads();
+    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[i] = tw[i];
+    for (int i = threadIdx.x; i < W; i += kRowThreads) a[P(bitrev(i, logw))] = Cx<T>{z[r0 * W + i], z[r1 * W + i]};
+    lds_barrier();
     fft_dit<T, false>(a, twl, W, logw, 1);
     const T h = T(0.5);
-    for (int k = threadIdx.x; k < nk; k += blockDim.x) {
+    for (int k = threadIdx.x; k < nk; k += kRowThreads) {
         const Cx<T> zk = a[P(k)];
         if (k == 0) {
             // the real bins A(0) = Re Z(0), A(W/2) = Re Z(W/2) (B: the imaginary parts) share
@@ -273,26 +297,29 @@ __global__ __launch_bounds__(256) void bv_rowfft_fwd(const T* z, Cx<T>* spec, co
 
 // nk = W/2 spectrum columns (column 0 = the packed real bins, see bv_rowfft_fwd), cw per
 // workgroup; the grid is mapped XCD-major (workgroup b runs on XCD b % 8) so the workgroups
-// that share the 128-byte lines of a spectrum row segment share one L2
+// that share the 128-byte lines of a spectrum row segment share one L2. (Persistent
+// workgroups with a register prefetch of the next block measured slower, 27.4 against 25.1 us.)
 template <typename T>
-__global__ __launch_bounds__(1024) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw, const T* ax, const T* ay, int nk,
-                                                    int H, int logh, int cw, T norm) {
+__global__ __launch_bounds__(kColThreads<T>) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw, const T* ax, const T* ay,
+                                                               int nk, int H, int logh, int logcw, T norm) {
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
+    const int cw = 1 << logcw;
     Cx<T>* twl = a + padded((size_t)cw * H);
     const int nblk = gridDim.x;
     const int blk = (nblk & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3));
     const int k0 = blk * cw;
     const int ncol = min(cw, nk - k0);
-    for (int i = threadIdx.x; i < H / 2; i += blockDim.x) twl[i] = tw[i];
-    for (int i = threadIdx.x; i < H * cw; i += blockDim.x) {
-        const int l = i / cw, c = i - l * cw;
-        if (c < ncol) a[P(c * H + bitrev(l, logh))] = spec[(int64_t)l * nk + k0 + c];
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int i = t; i < H / 2; i += nt) twl[i] = tw[i];
+    for (int i = t; i < H * cw; i += nt) {
+        const int l = i >> logcw, c = i & (cw - 1);
+        if (c < ncol) a[P((c << logh) + bitrev(l, logh))] = spec[(int64_t)l * nk + k0 + c];
     }
-    __syncthreads();
+    lds_barrier();
     fft_dit<T, false>(a, twl, H, logh, ncol);
-    for (int i = threadIdx.x; i < H * ncol; i += blockDim.x) {
-        const int c = i / H, l = i - c * H;
+    for (int i = t; i < H * ncol; i += nt) {
+        const int c = i >> logh, l = i & (H - 1);
         const int k = k0 + c;
         if (k == 0) {
             // packed column Z = C0 + i CN (C0, CN: spectra of the real bins' columns, both
@@ -312,43 +339,37 @@ __global__ __launch_bounds__(1024) void bv_colsolve(Cx<T>* spec, const Cx<T>* tw
         a[P(i)].x *= m;
         a[P(i)].y *= m;
     }
-    __syncthreads();
+    lds_barrier();
     fft_dif<T, true>(a, twl, H, logh, ncol);
-    for (int i = threadIdx.x; i < H * cw; i += blockDim.x) {
-        const int l = i / cw, c = i - l * cw;
-        if (c < ncol) spec[(int64_t)l * nk + k0 + c] = a[P(c * H + bitrev(l, logh))];
+    for (int i = t; i < H * cw; i += nt) {
+        const int l = i >> logcw, c = i & (cw - 1);
+        if (c < ncol) spec[(int64_t)l * nk + k0 + c] = a[P((c << logh) + bitrev(l, logh))];
     }
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void bv_rowfft_inv(const Cx<T>* spec, T* psi, const Cx<T>* tw, int W, int logw) {
+__global__ __launch_bounds__(kRowThreads) void bv_rowfft_inv(const Cx<T>* spec, T* psi, const Cx<T>* tw, int W, int logw) {
     extern __shared__ __align__(16) unsigned char smem[];
     Cx<T>* a = (Cx<T>*)smem;
     Cx<T>* twl = a + padded(W);
     const int nk = W / 2;  // column 0 packs the real bins: A(0) + i A(W/2)
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
-    for (int i = threadIdx.x; i < W / 2; i += blockDim.x) twl[i] = tw[i];
-    for (int k = threadIdx.x; k < W; k += blockDim.x) {
-        const bool lo = k <= nk;
-        const int kk = lo ? k : W - k;
-        Cx<T> A, B;
-        if (kk == 0 || kk == nk) {  // C2R: the real bins' imaginary parts are ignored
-            const Cx<T> a0 = spec[r0 * nk], b0 = spec[r1 * nk];
-            A = Cx<T>{kk == 0 ? a0.x : a0.y, T(0)};
-            B = Cx<T>{kk == 0 ? b0.x : b0.y, T(0)};
+    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[i] = tw[i];
+    // Z = A + i B over the Hermitian extension: bin k < W/2 gives Z(k) and Z(W - k); the real
+    // bins (C2R: their imaginary parts are ignored) give Z(0) and Z(W/2). Each bin read once.
+    for (int k = threadIdx.x; k < nk; k += kRowThreads) {
+        const Cx<T> A = spec[r0 * nk + k], B = spec[r1 * nk + k];
+        if (k == 0) {
+            a[P(0)] = Cx<T>{A.x, B.x};
+            a[P(nk)] = Cx<T>{A.y, B.y};
         } else {
-            A = spec[r0 * nk + kk];
-            B = spec[r1 * nk + kk];
+            a[P(k)] = Cx<T>{A.x - B.y, A.y + B.x};
+            a[P(W - k)] = Cx<T>{A.x + B.y, B.x - A.y};
         }
-        if (!lo) {
-            A.y = -A.y;
-            B.y = -B.y;
-        }
-        a[P(k)] = Cx<T>{A.x - B.y, A.y + B.x};  // Z = A + i B
     }
-    __syncthreads();
+    lds_barrier();
     fft_dif<T, true>(a, twl, W, logw, 1);
-    for (int i = threadIdx.x; i < W; i += blockDim.x) {
+    for (int i = threadIdx.x; i < W; i += kRowThreads) {
         const Cx<T> v = a[P(bitrev(i, logw))];
         psi[r0 * W + i] = v.x;
         psi[r1 * W + i] = v.y;
@@ -433,16 +454,16 @@ void poisson_lds(ws_bvort* b, const void* zin) {
     const int nk = b->W / 2;  // spectrum columns of the LDS path (real bins packed in column 0)
     Cx<T>* spec = (Cx<T>*)b->spec;
     const size_t row_lds = (padded(b->W) + b->W / 2) * cs, col_lds = (padded((size_t)b->cw * b->H) + b->H / 2) * cs;
-    hipLaunchKernelGGL((bv_rowfft_fwd<T>), dim3(b->H / 2), dim3(256), row_lds, b->stream, (const T*)zin, spec,
+    hipLaunchKernelGGL((bv_rowfft_fwd<T>), dim3(b->H / 2), dim3(kRowThreads), row_lds, b->stream, (const T*)zin, spec,
                        (const Cx<T>*)b->twW, b->W, b->logw);
     hck(hipGetLastError(), "bv_rowfft_fwd");
     // one radix-8 group per thread and pass
-    const int col_threads = std::min(1024, std::max(64, b->cw * b->H / 8));
-    hipLaunchKernelGGL((bv_colsolve<T>), dim3((nk + b->cw - 1) / b->cw), dim3(col_threads), col_lds,
-                       b->stream, spec, (const Cx<T>*)b->twH, (const T*)b->ax, (const T*)b->ay, nk, b->H, b->logh,
-                       b->cw, (T)(1.0 / ((double)b->W * b->H)));
+    const int col_threads = std::min(kColThreads<T>, std::max(64, b->cw * b->H / 8));
+    hipLaunchKernelGGL((bv_colsolve<T>), dim3((nk + b->cw - 1) / b->cw), dim3(col_threads), col_lds, b->stream, spec,
+                       (const Cx<T>*)b->twH, (const T*)b->ax, (const T*)b->ay, nk, b->H, b->logh,
+                       __builtin_ctz((unsigned)b->cw), (T)(1.0 / ((double)b->W * b->H)));
     hck(hipGetLastError(), "bv_colsolve");
-    hipLaunchKernelGGL((bv_rowfft_inv<T>), dim3(b->H / 2), dim3(256), row_lds, b->stream, (const Cx<T>*)spec,
+    hipLaunchKernelGGL((bv_rowfft_inv<T>), dim3(b->H / 2), dim3(kRowThreads), row_lds, b->stream, (const Cx<T>*)spec,
                        (T*)b->psi, (const Cx<T>*)b->twW, b->W, b->logw);
     hck(hipGetLastError(), "bv_rowfft_inv");
     b->launches += 3;
@@ -583,6 +604,8 @@ int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
                 const char* cwe = std::getenv("WS_BV_CW");
                 const size_t col_budget = cwe ? (size_t)std::atoi(cwe) * b->H * 2 * b->es() : 65536;
                 while (b->cw < 16 && (size_t)2 * b->cw * b->H * 2 * b->es() <= col_budget) b->cw *= 2;
+                // at most kColPer elements per thread of the column pass
+                while (b->cw > 1 && (size_t)b->cw * b->H > (size_t)(f64 ? 512 : 1024) * ws::kColPer) b->cw /= 2;
                 // data + twiddles can pass the 64 KB default of dynamic LDS (fp64 rows of 4096)
                 const int lds_max = 160 * 1024;
                 if (f64) {
