@@ -631,10 +631,28 @@ void autotune_time(ws_sim* s) {
     // final: the three fastest by best-of, timed again over longer windows (>= 16 launches,
     // 4 round-robin rounds, mean): best-of over short windows let one lucky window pick a
     // segment length a few % slower in a run (C2: seg 48 over 88, -4 %)
+    // plus the segment lengths next to the best one (+-8, +-16 rows: the march constraint
+    // seg + 2 cone = 0 mod 8 keeps them valid) when the heuristic list skipped them
+    {
+        const Cand b = *std::min_element(cands.begin(), cands.end(),
+                                         [](const Cand& x, const Cand& y) { return x.ms < y.ms; });
+        if (!s->seg_fixed)
+            for (int d : {-16, -8, 8, 16}) {
+                const int seg = b.seg + d;
+                if (seg < 8 || seg > s->slot[0]->H) continue;
+                const bool have = std::any_of(cands.begin(), cands.end(), [&](const Cand& c) {
+                    return c.kernel == b.kernel && c.tb == b.tb && c.align == b.align && c.seg == seg;
+                });
+                if (!have) cands.push_back({b.kernel, seg, b.align, b.tb, 0.f});
+            }
+    }
     std::vector<Cand*> top;
     for (Cand& c : cands) top.push_back(&c);
     std::sort(top.begin(), top.end(), [](const Cand* a, const Cand* b) { return a->ms < b->ms; });
-    if (top.size() > 3) top.resize(3);
+    // the new neighbours (ms = 0) sort first; keep them and the three fastest timed ones
+    size_t keep = 0;
+    while (keep < top.size() && top[keep]->ms == 0.f) ++keep;
+    if (top.size() > keep + 3) top.resize(keep + 3);
     if (top.size() > 1) {
         std::vector<float> sum(top.size(), 0.f);
         const int long_reps = std::max(reps, 16);
