@@ -17,6 +17,8 @@
 // stage update (and the RK4 accumulator) in the same pass.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <string>
 
 #include "ws_abi.h"
@@ -40,6 +42,8 @@ struct LpeArgs {
     const T *bu, *bv, *bh;  // state at the start of the step
     T *ou, *ov, *oh;        // base + c * k
     T *au, *av, *ah;        // RK4 accumulator
+    const T* tin;           // total thickness sum_k h_k of the input (H x W), or null: summed here
+    T* tout;                // total thickness of the output h (summed in the walk), or null
     int W, H, L;
     int64_t lstride;        // H * W
     T c, w;
@@ -102,8 +106,13 @@ void lpe_stage_kernel(LpeArgs<T> a) {
         hc[i] = a.h + (int64_t)gy * a.W + gx;
         T t = T(0);
         if (c < kCX * kCY) {
+            if (a.tin) {
+                // the producing stage summed the levels in the same order (bitwise the same)
+                t = a.tin[(int64_t)gy * a.W + gx];
+            } else {
 #pragma unroll 8
-            for (int k = 0; k < a.L; ++k) t = t + hc[i][(int64_t)k * a.lstride];
+                for (int k = 0; k < a.L; ++k) t = t + hc[i][(int64_t)k * a.lstride];
+            }
         }
         total[i] = t;
         prefix[i] = T(0);
@@ -116,6 +125,7 @@ void lpe_stage_kernel(LpeArgs<T> a) {
     const int64_t oc = (int64_t)yc * a.W + xc;
     const int64_t oe = (int64_t)yc * a.W + wrapi(xc + 1, a.W), ow = (int64_t)yc * a.W + wrapi(xc - 1, a.W);
     const int64_t on = (int64_t)wrapi(yc + 1, a.H) * a.W + xc, os = (int64_t)wrapi(yc - 1, a.H) * a.W + xc;
+    T tsum = T(0);  // total thickness of the output column, levels in order (as the scan sums)
     for (int k0 = 0; k0 < a.L; k0 += kChunk) {
         const int nk = a.L - k0 < kChunk ? a.L - k0 : kChunk;
 #pragma unroll
@@ -171,12 +181,16 @@ void lpe_stage_kernel(LpeArgs<T> a) {
                 if (a.acc_mode == 3) {
                     a.ou[o] = b0 + a.c * (a.au[o] + du);
                     a.ov[o] = b1 + a.c * (a.av[o] + dv);
-                    a.oh[o] = b2 + a.c * (a.ah[o] + dh);
+                    const T hnew = b2 + a.c * (a.ah[o] + dh);
+                    a.oh[o] = hnew;
+                    tsum = tsum + hnew;
                     continue;
                 }
                 a.ou[o] = b0 + a.c * du;
                 a.ov[o] = b1 + a.c * dv;
-                a.oh[o] = b2 + a.c * dh;
+                const T hnew = b2 + a.c * dh;
+                a.oh[o] = hnew;
+                tsum = tsum + hnew;
                 if (a.acc_mode == 1) {
                     a.au[o] = a.w * du;
                     a.av[o] = a.w * dv;
@@ -190,6 +204,7 @@ void lpe_stage_kernel(LpeArgs<T> a) {
         }
         __syncthreads();  // the next chunk overwrites Ms
     }
+    if (a.tout && inside) a.tout[oc] = tsum;
 }
 
 void hck(hipError_t e, const char* what) {
@@ -209,6 +224,11 @@ struct ws_lpe {
     void* A[3] = {};
     void* B[3] = {};
     void* acc[3] = {};
+    // total thickness (sum over levels of h, H x W) of S[0], S[1], A, B, written by the stage
+    // that produces the set, so the next stage's column scan skips its pre-pass over h;
+    // tot_ok[i] false (initial / set_field state) = the stage sums it itself
+    void* tot[4] = {};
+    bool tot_ok[4] = {};
     int cur = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
@@ -227,15 +247,32 @@ void lpe_free(ws_lpe* m) {
     for (void** grp : {m->A, m->B, m->acc})
         for (int i = 0; i < 3; ++i)
             if (grp[i]) (void)hipFree(grp[i]);
+    for (void* p : m->tot)
+        if (p) (void)hipFree(p);
     for (hipEvent_t e : {m->ev0, m->ev1})
         if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
 }
 
+// index of a field set's total-thickness buffer: S[0], S[1], A, B
+int tot_index(const ws_lpe* m, void* const* set) {
+    if (set == m->S[0]) return 0;
+    if (set == m->S[1]) return 1;
+    return set == m->A ? 2 : 3;
+}
+
 template <typename T>
 void stage(ws_lpe* m, void* const* in, void* const* out, T c, T w, int acc_mode) {
     LpeArgs<T> a{};
+    const int ti = tot_index(m, in), to = tot_index(m, out);
+    static const bool carry = [] {
+        const char* e = std::getenv("WS_LPE_TOTALS");  // 0: every stage sums the thickness itself
+        return !(e && std::atoi(e) == 0);
+    }();
+    a.tin = carry && m->tot_ok[ti] ? (const T*)m->tot[ti] : nullptr;
+    a.tout = (T*)m->tot[to];
+    m->tot_ok[to] = true;
     a.u = (const T*)in[0];
     a.v = (const T*)in[1];
     a.h = (const T*)in[2];
@@ -337,6 +374,7 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
                 }
             for (void** grp : {m->A, m->B, m->acc})
                 for (int i = 0; i < 3; ++i) ws::hck(hipMalloc(&grp[i], fb), "hipMalloc");
+            for (void*& p : m->tot) ws::hck(hipMalloc(&p, (size_t)m->H * m->W * m->es()), "hipMalloc");
         } catch (...) {
             ws::lpe_free(m);
             throw;
@@ -361,6 +399,7 @@ int ws_lpe_set_field(ws_lpe_t* m, int32_t field, const void* host, int32_t level
         ws::abi_set_device(m->device);
         ws::hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
         ws::hck(hipMemcpy(m->S[m->cur][field], host, m->cells() * m->es(), hipMemcpyHostToDevice), "hipMemcpy");
+        m->tot_ok[m->cur] = false;  // the next stage sums the new thickness itself
     });
 }
 

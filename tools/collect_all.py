@@ -1,0 +1,23 @@
+"""Collect tools/measure_all.sh's bench lines (gpurun_out/all/<cfg>_<method>.json) into one
+profiles/ summary: python3 tools/collect_all.py gpurun_out/all profiles/r02_all_configs.json"""
+import glob
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+out = {"note": "one MI355X, tools/measure_all.sh (300 warm-up + 200 timed steps, autotuned); achieved = 6 words "
+               "per cell-update x cell-updates per launch / mean launch time (bench.py byte_model; the physics "
+               "modes: their own words-per-cell models, DESIGN.md sections 10-11)",
+       "configs": {}}
+for f in sorted(glob.glob(os.path.join(src, "*.json"))):
+    d = json.load(open(f))
+    r = d["roofline"]
+    out["configs"][os.path.basename(f)[:-5]] = {
+        "value": d["value"], "ms_per_step": d["ms_per_step"], "kernel": r.get("kernel"),
+        "seg_rows": r.get("seg_rows"), "strip_out_cols": r.get("strip_out_cols"),
+        "steps_per_launch": r.get("steps_per_launch"), "mean_launch_ms": r.get("mean_launch_ms"),
+        "achieved_gbs": r.get("achieved"), "frac": r.get("frac"), "bytes_per_launch": r.get("bytes_per_launch"),
+        "cfl": (d.get("cfl") or {}).get("value")}
+json.dump(out, open(dst, "w"), indent=1)
+print(len(out["configs"]), "configs ->", dst)
