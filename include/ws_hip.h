@@ -212,7 +212,10 @@ int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]);
 /* One rank of a y-slab decomposition of the global grid described by cfg. Rank r owns
  * rows [row0, row0 + rows) (balanced split, returned); halo rows are exchanged with
  * ncclSend/ncclRecv between neighbouring ranks. Fields set / read through the slab's
- * grids are the local rows only. Results are bitwise identical to one GPU. */
+ * grids are the local rows only. Results are bitwise identical to one GPU.
+ * id == NULL (measurement aid): the slab gets no communicator -- its halo exchanges are
+ * skipped and the halo rows keep what they hold -- so one process can time one rank's
+ * compute schedule of an N-rank decomposition on one GPU (results then differ). */
 int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
                        ws_sim_t** out, int32_t* row0, int32_t* rows);
 
@@ -329,6 +332,14 @@ int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows
  * runs only inside run(k >= 2), inside a slab block with room for both steps, and with the
  * configured spacing on both grids; results are identical to two one-step launches. */
 int ws_sim_steps_per_launch(const ws_sim_t* sim, int32_t* steps);
+
+/* Slab schedule (new: the reference has no distributed path): block = time steps per halo
+ * exchange (deep halo of block x NST rows; 1 for a whole domain), overlap = 1 when run()
+ * uses the overlap schedule -- each block's edge bands (the rows the neighbours need) on a
+ * second HIP stream followed there by the halo exchange, the interior rows meanwhile on the
+ * compute stream (bit-identical to the stream-ordered schedule). Default: overlap when the
+ * thinnest slab has at least 3 x block x NST rows; WS_SLAB_OVERLAP=0|1 fixes it. */
+int ws_sim_slab_schedule(const ws_sim_t* sim, int32_t* block, int32_t* overlap);
 
 /* CFL number of the current state (new: the reference's dt is fixed and it has no CFL):
  * max over cells of max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy), computed in

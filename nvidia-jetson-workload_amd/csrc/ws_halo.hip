@@ -28,6 +28,22 @@ HaloPlan make_halo_plan(const Geom& g, int elem_size, int rank, int nranks, int 
     return p;
 }
 
+namespace {
+__global__ void delay_kernel(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+}  // namespace
+
+hipError_t emulated_transfer(double us, hipStream_t s) {
+    int dev = 0, khz = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, (uint64_t)(us * khz / 1000.0));
+    return hipGetLastError();
+}
+
 std::vector<HaloXfer> HaloPlan::xfers() const {
     std::vector<HaloXfer> out;
     for (int side = 0; side < 2; ++side) {

@@ -263,6 +263,13 @@ struct ws_sim {
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
     int32_t want_blocks_override = 0;  // WS_WANT_BLOCKS
+    // slab overlap schedule (overlap_block): a block's edge bands run on `edge`, the halo
+    // exchange follows them there, the interior runs meanwhile on `stream`
+    bool overlap = false;
+    hipStream_t edge = nullptr;
+    hipEvent_t ev_edge = nullptr, ev_join = nullptr;
+    ws_grid* ov[4] = {};      // interior ping-pong (0, 1), edge-band ping-pong (2, 3); u, v, h
+    double emu_xfer_us = -1.0;  // no communicator (measurement aid): WS_EMU_XFER_US, see slab_exchange
     // slab decomposition
     ws::SlabComm* comm = nullptr;
     ws::HaloStaging* staging = nullptr;  // slab of a group: its halo messages (group_exchange)
@@ -338,6 +345,8 @@ int fused_stages(const ws_sim* s) {
 }
 
 bool use_fused(const ws_sim* s) { return s->fused && s->slot[0]->W >= 2; }
+
+void slab_exchange(ws_sim* s, ws_grid* g, int nfields, int depth, hipStream_t st);
 
 // Output rows of a fused launch: [y0, y1) (empty if y1 <= y0).
 struct RowRange {
@@ -415,7 +424,7 @@ void step_begin(ws_sim* s, int nsteps = 1) {
         // h: the compulsory traffic of one step) x the cell-updates it performs
         s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L * nsteps, s->stream);
         // slab: at a block start, the block's halo (group slabs: copied by group_step)
-        if (s->block_pos == 0 && s->comm) s->comm->exchange(c->f, 3, (int)sizeof(T), g, s->block * nst, s->stream);
+        if (s->block_pos == 0) slab_exchange(s, c, 3, s->block * nst, s->stream);
         fused_launch<T>(s, nst, nsteps, step_rows(s, nst, nsteps), {0, 0}, s->seg_rows(nst));
         return;
     }
@@ -452,12 +461,22 @@ void step_begin(ws_sim* s, int nsteps = 1) {
 // of two steps back instead of one -- visible only through a grid handle held across run(),
 // DESIGN.md deviation D6.)
 template <typename T>
+void rotate(ws_sim* s, int nsteps);
+
+template <typename T>
 void step_end(ws_sim* s, int nsteps = 1) {
-    const T dt = (T)s->dt;
     if (use_fused(s)) {
         s->timer.end(s->stream);
         s->block_pos = (s->block_pos + nsteps) % s->block;
     }
+    rotate<T>(s, nsteps);
+}
+
+// After nsteps steps written into the next grid: the PE T / P update (nsteps updates in one
+// pass) and the reference's grid rotation.
+template <typename T>
+void rotate(ws_sim* s, int nsteps) {
+    const T dt = (T)s->dt;
     ws_grid* c = s->slot[s->cur];
     ws_grid* n = s->slot[1 - s->cur];
     const bool pe = s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS;
@@ -490,13 +509,39 @@ void step_end(ws_sim* s, int nsteps = 1) {
 // Steps the next launch advances, of `remaining`: 2 when the tuned configuration launches
 // two steps at once, the slab block has room for both, and both steps see the config's
 // spacing (the kernel's later stages use it); else 1.
+// The halo exchange of a slab: RCCL (ws_comm.cpp), or -- a slab created without a
+// communicator, the measurement aid of ws_sim_create_slab -- the pack / unpack kernels
+// around a WS_EMU_XFER_US wall-clock wait in place of the transfer (the halo rows then hold
+// the slab's own edge rows: timing only).
+void slab_exchange(ws_sim* s, ws_grid* g, int nfields, int depth, hipStream_t st) {
+    if (s->comm) {
+        s->comm->exchange(g->f, nfields, (int)elem_size(s->dtype), g->geom(), depth, st);
+        return;
+    }
+    if (s->nranks < 2 || s->emu_xfer_us < 0 || s->in_group) return;
+    const ws::HaloPlan plan = ws::make_halo_plan(g->geom(), (int)elem_size(s->dtype), s->rank, s->nranks, nfields, depth);
+    if (!s->staging) s->staging = new ws::HaloStaging;
+    s->staging->ensure(plan.msg_bytes());
+    ws::HaloFields hf{};
+    for (int f = 0; f < nfields; ++f) hf.f[f] = (char*)g->f[f];
+    for (int side = 0; side < 2; ++side)
+        if (plan.has[side]) WS_HIP_CHECK(ws::halo_pack(plan, hf, side, s->staging->send[side], st));
+    WS_HIP_CHECK(ws::emulated_transfer(s->emu_xfer_us, st));
+    for (int side = 0; side < 2; ++side)
+        if (plan.has[side]) WS_HIP_CHECK(ws::halo_unpack(plan, hf, side, s->staging->send[side], st));
+}
+
+bool config_spacing(const ws_sim* s) {
+    const double dx = to_prec(s->cfg.dx, s->dtype), dy = to_prec(s->cfg.dy, s->dtype);
+    for (const ws_grid* g : {s->slot[0], s->slot[1]})
+        if (g->dx != dx || g->dy != dy) return false;
+    return true;
+}
+
 int launch_steps(const ws_sim* s, int remaining) {
     if (remaining < 2 || !use_fused(s) || s->launch_tb() < 2) return 1;
     if (s->nranks > 1 && s->block_pos + 2 > s->block) return 1;  // a slab's block (one domain: no blocks)
-    const double dx = to_prec(s->cfg.dx, s->dtype), dy = to_prec(s->cfg.dy, s->dtype);
-    for (const ws_grid* g : {s->slot[0], s->slot[1]})
-        if (g->dx != dx || g->dy != dy) return 1;
-    return 2;
+    return config_spacing(s) ? 2 : 1;
 }
 
 // One time step on the stream (no host synchronisation).
@@ -504,6 +549,143 @@ template <typename T>
 void enqueue_steps(ws_sim* s, int nsteps) {
     step_begin<T>(s, nsteps);
     step_end<T>(s, nsteps);
+}
+
+// ------------------------------------------------------------------------------------
+// Slab overlap schedule (north_star: the halo exchange overlapped with interior compute on a
+// second HIP stream). A block of `steps` steps (one halo exchange, depth D = steps x NST
+// rows, as in the stream-ordered schedule above) is split by rows:
+//   * edge bands, on the slab's `edge` stream: the rows within 2D of a non-global side,
+//     advanced the whole block through their own ping-pong grids (ov[2], ov[3]); launch j
+//     (cumulative cone C_j) computes rows [C_j - D, 2D - C_j) at the top and
+//     [H - 2D + C_j, H + D - C_j) at the bottom, so the last launch writes exactly rows
+//     [0, D) and [H - D, H) of the next grid -- the rows the neighbours need. The exchange of
+//     the next block's halo follows on the same stream;
+//   * interior, on the compute stream meanwhile: launch j computes rows [C_j, H - C_j)
+//     through ov[0], ov[1]; it reads only owned rows (never the halo), and its last launch
+//     writes rows [D, H - D) of the next grid.
+// Every launch reads exactly the rows its predecessor in the same band wrote (the
+// dependency cone shrinks by the launch's NST x steps per side), so both parts are
+// bit-identical to the stream-ordered schedule. Two cross-stream waits per block: the edge
+// launches of block k read rows [D, 2D) that the interior of block k-1 wrote (ev_join), and
+// the interior of block k reads rows [0, D) that the edges of block k-1 wrote (ev_edge). The
+// exchange itself is waited on only by the next block's edges (stream order on `edge`).
+// ------------------------------------------------------------------------------------
+
+// steps per launch within a block (2 while the tuned configuration launches two at once)
+std::vector<int> block_launches(const ws_sim* s, int steps) {
+    const bool two = use_fused(s) && s->launch_tb() >= 2 && config_spacing(s);
+    std::vector<int> n;
+    for (int left = steps; left > 0;) {
+        const int k = two && left >= 2 ? 2 : 1;
+        n.push_back(k);
+        left -= k;
+    }
+    return n;
+}
+
+// launch j's interior rows and edge-band rows (two ranges; merged into A when they touch)
+struct BandRows {
+    RowRange interior, A, B;
+};
+
+BandRows band_rows(const ws_grid* g, int C, int D) {
+    const int H = g->H;
+    const int lo = g->top_clamp ? 0 : C - D, hi = g->bot_clamp ? H : H + D - C;
+    BandRows r{{g->top_clamp ? 0 : C, g->bot_clamp ? H : H - C}, {0, 0}, {0, 0}};
+    RowRange top{0, 0}, bot{0, 0};
+    if (!g->top_clamp) top = {lo, std::min(hi, 2 * D - C)};
+    if (!g->bot_clamp) bot = {std::max(lo, H - 2 * D + C), hi};
+    if (top.rows() > 0 && bot.rows() > 0 && top.y1 >= bot.y0) {
+        r.A = {top.y0, bot.y1};
+    } else {
+        r.A = top.rows() > 0 ? top : bot;
+        r.B = top.rows() > 0 ? bot : RowRange{0, 0};
+    }
+    return r;
+}
+
+// the overlap grids (allocated on first use; same layout and slab flags as the slots)
+void ensure_overlap_grids(ws_sim* s) {
+    if (!s->edge) {
+        // (a high-priority edge stream measured no different: tools/rank_timing.py)
+        WS_HIP_CHECK(hipStreamCreateWithFlags(&s->edge, hipStreamNonBlocking));
+        WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
+        WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    }
+    const ws_grid* c = s->slot[0];
+    for (auto& g : s->ov) {
+        if (g) continue;
+        g = new_grid(c->W, c->H, c->L, s->dtype, s->device, 3, s->stream);
+        g->owned = true;
+        g->dx = c->dx; g->dy = c->dy;
+        g->top_clamp = c->top_clamp; g->bot_clamp = c->bot_clamp;
+        g->row0 = c->row0; g->gH = c->gH;
+    }
+}
+
+// Phase 1 (compute stream): join the previous block and hand the edge stream its start.
+void overlap_begin(ws_sim* s, bool first) {
+    if (!first) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // rows [0, D) of block k-1
+    WS_HIP_CHECK(hipEventRecord(s->ev_join, s->stream));
+    WS_HIP_CHECK(hipStreamWaitEvent(s->edge, s->ev_join, 0));
+}
+
+// Phase 2 (edge stream): the edge bands of the block; ev_edge marks them done.
+template <typename T>
+void overlap_edges(ws_sim* s, int steps) {
+    const int nst = fused_stages(s), D = steps * nst;
+    const std::vector<int> n = block_launches(s, steps);
+    ws_grid* in = s->slot[s->cur];
+    int C = 0;
+    for (size_t j = 0; j < n.size(); ++j) {
+        C += n[j] * nst;
+        ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[2 + j % 2];
+        const BandRows r = band_rows(in, C, D);
+        // the tuned segment rows (one segment per band -- fewer warm-up rows, longer marches
+        // -- measured no faster: the edges are on the critical path at 8 slabs)
+        fused_launch<T>(s, nst, n[j], r.A, r.B, s->seg_rows(nst), s->edge, in, out);
+        in = out;
+    }
+    WS_HIP_CHECK(hipEventRecord(s->ev_edge, s->edge));
+}
+
+// Phase 3 (compute stream): the interior of the block, then the PE T / P update and rotation.
+template <typename T>
+void overlap_interior(ws_sim* s, int steps) {
+    const int nst = fused_stages(s), D = steps * nst;
+    const std::vector<int> n = block_launches(s, steps);
+    ws_grid* in = s->slot[s->cur];
+    const ws::Geom g = in->geom();
+    int C = 0;
+    for (size_t j = 0; j < n.size(); ++j) {
+        C += n[j] * nst;
+        ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[j % 2];
+        const BandRows r = band_rows(in, C, D);
+        s->timer.begin(0, 6.0 * sizeof(T) * g.W * r.interior.rows() * g.L * n[j], s->stream);
+        fused_launch<T>(s, nst, n[j], r.interior, {0, 0}, s->seg_rows(nst), s->stream, in, out);
+        s->timer.end(s->stream);
+        in = out;
+    }
+    rotate<T>(s, steps);
+}
+
+// Whether run() uses the overlap schedule: a slab of the fused path whose grids all have the
+// configured spacing (the two-step launches' later stages assume it).
+// (A one-rank RCCL slab runs it only when WS_SLAB_OVERLAP=1: no edge bands, no-op exchanges.)
+bool overlap_active(const ws_sim* s) {
+    return s->overlap && (s->nranks > 1 || s->comm) && use_fused(s) && config_spacing(s);
+}
+
+// One overlapped block of a slab with an RCCL communicator.
+template <typename T>
+void overlap_block(ws_sim* s, int steps, bool first, bool last) {
+    const int depth = s->block * fused_stages(s);
+    if (first) slab_exchange(s, s->slot[s->cur], 3, depth, s->stream);
+    overlap_begin(s, first);
+    overlap_edges<T>(s, steps);
+    if (!last) slab_exchange(s, s->slot[1 - s->cur], 3, depth, s->edge);  // the next block's halo, behind the edge bands
+    overlap_interior<T>(s, steps);
 }
 
 template <typename T>
@@ -805,16 +987,26 @@ void run_steps(ws_sim* s, int k) {
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
     }
+    const bool ovl = k > 0 && overlap_active(s);
+    if (ovl) ensure_overlap_grids(s);
     for (int i = 0; i < k;) {
-        const int n = launch_steps(s, k - i);
-        if (s->dtype == WS_F64) enqueue_steps<double>(s, n);
-        else enqueue_steps<float>(s, n);
+        // overlap schedule: one block per iteration; else one launch
+        const int n = ovl ? std::min(s->block, k - i) : launch_steps(s, k - i);
+        if (ovl) {
+            if (s->dtype == WS_F64) overlap_block<double>(s, n, i == 0, i + n == k);
+            else overlap_block<float>(s, n, i == 0, i + n == k);
+        } else if (s->dtype == WS_F64) {
+            enqueue_steps<double>(s, n);
+        } else {
+            enqueue_steps<float>(s, n);
+        }
         for (int j = 0; j < n; ++j) {
             s->time = s->dtype == WS_F64 ? advance_time<double>(s->time, s->dt) : advance_time<float>(s->time, s->dt);
             s->step++;
         }
         i += n;
     }
+    if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     if (s->aux_active) {
         WS_HIP_CHECK(hipEventRecord(s->aux_out, s->aux));
         WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->aux_out, 0));
@@ -847,11 +1039,12 @@ void run_steps(ws_sim* s, int k) {
 }
 
 void sim_free(ws_sim* s) {
-    for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
+    for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3, s->ov[0], s->ov[1], s->ov[2], s->ov[3]})
         if (g) { grid_free(g); delete g; }
-    for (hipEvent_t e : {s->ev0, s->ev1, s->aux_in, s->aux_out})
+    for (hipEvent_t e : {s->ev0, s->ev1, s->aux_in, s->aux_out, s->ev_edge, s->ev_join})
         if (e) (void)hipEventDestroy(e);
     if (s->aux) (void)hipStreamDestroy(s->aux);
+    if (s->edge) (void)hipStreamDestroy(s->edge);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
     if (s->cfl_scratch) (void)hipFree(s->cfl_scratch);
     delete s->comm;
@@ -935,7 +1128,17 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             const int thin = cfg->grid_height / slab.nranks;
             s->block = std::max(1, std::min(6, std::min(ws::kHalo, thin) / nst));
             if (const char* e = std::getenv("WS_SLAB_BLOCK")) s->block = std::max(1, std::min(s->block, std::atoi(e)));
+            // overlap schedule (overlap_block) when the slabs are deep: its edge bands cost ~11 %
+            // more stencil work plus two cross-stream waits per block, which the hidden
+            // exchange repays at C2's 4 slabs (1024 rows: 0.044 -> 0.039 ms/step with a 40 us
+            // transfer) but not surely at 8 (512 rows: break-even near 60-80 us per exchange;
+            // tools/rank_timing.py). Every rank decides alike (global quantities).
+            s->overlap = thin >= 32 * s->block * nst;
+            if (const char* e = std::getenv("WS_SLAB_OVERLAP")) s->overlap = std::atoi(e) != 0;
+        } else if (comm && s->fused) {
+            s->overlap = env_int("WS_SLAB_OVERLAP", 0) != 0;
         }
+        if (!comm && slab.nranks > 1 && std::getenv("WS_EMU_XFER_US")) s->emu_xfer_us = std::atof(std::getenv("WS_EMU_XFER_US"));
         if (!s->fused && method != WS_EULER) s->tmpA = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
         if (!s->fused && method == WS_RK4) {
             s->tmpB = new_grid(W, H, L, s->dtype, s->device, 3, s->stream);
@@ -1483,7 +1686,7 @@ int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]) {
 int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
                        ws_sim_t** out, int32_t* row0, int32_t* rows) {
     return guarded([&] {
-        require(cfg && id && out, WS_ERR_INVALID, "null pointer");
+        require(cfg && out, WS_ERR_INVALID, "null pointer");
         require(nranks >= 1 && rank >= 0 && rank < nranks, WS_ERR_INVALID, "bad rank / nranks");
         require(cfg->grid_height >= nranks, WS_ERR_INVALID, "fewer rows than ranks");
         int r0 = 0, nrows = 0;
@@ -1493,7 +1696,8 @@ int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, con
         set_device(cfg->device_id);
         // a 1-rank slab still gets its communicator: same code path as N>1 (the exchanges
         // are no-ops), so a 1-GPU run exercises the RCCL bootstrap
-        ws::SlabComm* comm = new ws::SlabComm(rank, nranks, id);
+        // (id == NULL: no communicator, exchanges skipped -- the measurement aid of ws_hip.h)
+        ws::SlabComm* comm = id ? new ws::SlabComm(rank, nranks, id) : nullptr;
         ws_sim* s = nullptr;
         try {
             SlabInfo si;
@@ -1613,6 +1817,14 @@ int ws_sim_steps_per_launch(const ws_sim_t* s, int32_t* steps) {
     });
 }
 
+int ws_sim_slab_schedule(const ws_sim_t* s, int32_t* block, int32_t* overlap) {
+    return guarded([&] {
+        require(s != nullptr && block != nullptr && overlap != nullptr, WS_ERR_INVALID, "null pointer");
+        *block = s->block;
+        *overlap = overlap_active(s) ? 1 : 0;
+    });
+}
+
 int ws_sim_set_numerics(ws_sim_t* s, int32_t mode) {
     return guarded([&] {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
@@ -1680,6 +1892,10 @@ int ws_sim_comm_barrier(ws_sim_t* s) {
 struct ws_group {
     std::vector<ws_sim*> slabs;
     hipStream_t stream = nullptr;
+    // overlap schedule: the transport between the slabs' edge streams (what RCCL does on each
+    // rank's edge stream), created on first use
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_x = nullptr;
     int device = 0;
 };
 
@@ -1689,32 +1905,55 @@ namespace {
 // its neighbour messages (halo_pack), the messages move by device copies into the
 // neighbours' receive staging (what RCCL does between processes, ws_comm.cpp), and each slab
 // unpacks them -- the same plan and kernels as the multi-process path.
-void group_exchange(ws_group* gr, int nfields, int depth) {
+void group_exchange(ws_group* gr, int nfields, int depth, bool next = false, hipStream_t st = nullptr) {
+    if (!st) st = gr->stream;
     const int n = (int)gr->slabs.size();
     std::vector<ws::HaloPlan> plans(n);
     std::vector<ws::HaloFields> hf(n);
     for (int r = 0; r < n; ++r) {
         ws_sim* s = gr->slabs[r];
-        const ws_grid* me = s->slot[s->cur];
+        const ws_grid* me = s->slot[next ? 1 - s->cur : s->cur];
         plans[r] = ws::make_halo_plan(me->geom(), (int)elem_size(me->dtype), r, n, nfields, depth);
         if (!s->staging) s->staging = new ws::HaloStaging;
         s->staging->ensure(plans[r].msg_bytes());
         for (int f = 0; f < nfields; ++f) hf[r].f[f] = (char*)me->f[f];
         for (int side = 0; side < 2; ++side)
             if (plans[r].has[side])
-                WS_HIP_CHECK(ws::halo_pack(plans[r], hf[r], side, s->staging->send[side], gr->stream));
+                WS_HIP_CHECK(ws::halo_pack(plans[r], hf[r], side, s->staging->send[side], st));
     }
     for (int r = 0; r < n; ++r)
         for (int side = 0; side < 2; ++side) {
             if (!plans[r].has[side]) continue;
             ws_sim* peer = gr->slabs[plans[r].peer[side]];
             WS_HIP_CHECK(hipMemcpyAsync(peer->staging->recv[1 - side], gr->slabs[r]->staging->send[side],
-                                        (size_t)plans[r].msg_bytes(), hipMemcpyDeviceToDevice, gr->stream));
+                                        (size_t)plans[r].msg_bytes(), hipMemcpyDeviceToDevice, st));
         }
     for (int r = 0; r < n; ++r)
         for (int side = 0; side < 2; ++side)
             if (plans[r].has[side])
-                WS_HIP_CHECK(ws::halo_unpack(plans[r], hf[r], side, gr->slabs[r]->staging->recv[side], gr->stream));
+                WS_HIP_CHECK(ws::halo_unpack(plans[r], hf[r], side, gr->slabs[r]->staging->recv[side], st));
+}
+
+// One overlapped block of every slab (overlap_block with the group's device-copy transport
+// on xstream between the slabs' edge streams).
+template <typename T>
+void group_overlap_block(ws_group* gr, int steps, bool first, bool last) {
+    ws_sim* s0 = gr->slabs[0];
+    const int depth = s0->block * fused_stages(s0);
+    if (first) group_exchange(gr, 3, depth);
+    for (ws_sim* s : gr->slabs) overlap_begin(s, first);
+    for (ws_sim* s : gr->slabs) overlap_edges<T>(s, steps);
+    if (!last) {
+        if (!gr->xstream) {
+            WS_HIP_CHECK(hipStreamCreateWithFlags(&gr->xstream, hipStreamNonBlocking));
+            WS_HIP_CHECK(hipEventCreateWithFlags(&gr->ev_x, hipEventDisableTiming));
+        }
+        for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(gr->xstream, s->ev_edge, 0));
+        group_exchange(gr, 3, depth, true, gr->xstream);
+        WS_HIP_CHECK(hipEventRecord(gr->ev_x, gr->xstream));
+        for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(s->edge, gr->ev_x, 0));
+    }
+    for (ws_sim* s : gr->slabs) overlap_interior<T>(s, steps);
 }
 
 template <typename T>
@@ -1767,6 +2006,8 @@ int ws_group_destroy(ws_group_t* gr) {
         (void)hipStreamSynchronize(gr->stream);
         for (ws_sim* s : gr->slabs) sim_free(s);
         (void)hipStreamDestroy(gr->stream);
+        if (gr->xstream) (void)hipStreamDestroy(gr->xstream);
+        if (gr->ev_x) (void)hipEventDestroy(gr->ev_x);
         delete gr;
     });
 }
@@ -1800,10 +2041,17 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
         }
         for (ws_sim* s : gr->slabs) s->block_pos = 0;
         WS_HIP_CHECK(hipEventRecord(s0->ev0, gr->stream));
+        bool ovl = k > 0;  // every slab must agree
+        for (ws_sim* s : gr->slabs) ovl = ovl && overlap_active(s);
+        if (ovl)
+            for (ws_sim* s : gr->slabs) ensure_overlap_grids(s);
         for (int i = 0; i < k;) {
             int n = 2;  // every slab must agree (they share the block position and the choice)
             for (ws_sim* s : gr->slabs) n = std::min(n, launch_steps(s, k - i));
-            if (s0->dtype == WS_F64) group_step<double>(gr, n);
+            if (ovl) n = std::min(s0->block, k - i);
+            if (ovl && s0->dtype == WS_F64) group_overlap_block<double>(gr, n, i == 0, i + n == k);
+            else if (ovl) group_overlap_block<float>(gr, n, i == 0, i + n == k);
+            else if (s0->dtype == WS_F64) group_step<double>(gr, n);
             else group_step<float>(gr, n);
             for (ws_sim* s : gr->slabs)
                 for (int j = 0; j < n; ++j) {
@@ -1812,6 +2060,8 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
                 }
             i += n;
         }
+        if (ovl)
+            for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(gr->stream, s->ev_edge, 0));
         WS_HIP_CHECK(hipEventRecord(s0->ev1, gr->stream));
         if (k > 0) {  // seam diagnostics need the neighbours' current rows (see run_steps)
             group_exchange(gr, 2, 1);

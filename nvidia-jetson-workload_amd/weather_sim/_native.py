@@ -124,6 +124,7 @@ SIGNATURES = {
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
     "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
     "ws_sim_steps_per_launch": [_P, _PI],
+    "ws_sim_slab_schedule": [_P, _PI, _PI],
     "ws_sim_cfl": [_P, _PD, _PD, _I, _PD],
     "ws_sim_set_numerics": [_P, _I],
     "ws_sim_get_numerics": [_P, _PI],

@@ -534,7 +534,8 @@ class WeatherSimulation:
         else:
             rank, nranks, uid = _slab
             r0, nr = ctypes.c_int32(), ctypes.c_int32()
-            idbuf = (ctypes.c_uint8 * _native.COMM_ID_BYTES).from_buffer_copy(uid)
+            # uid None: no communicator (measurement aid, ws_hip.h ws_sim_create_slab)
+            idbuf = None if uid is None else (ctypes.c_uint8 * _native.COMM_ID_BYTES).from_buffer_copy(uid)
             check(lib.ws_sim_create_slab(ctypes.byref(c), int(rank), int(nranks), idbuf, ctypes.byref(h),
                                          ctypes.byref(r0), ctypes.byref(nr)))
             self.row0, self.rows = r0.value, nr.value
@@ -697,6 +698,13 @@ class WeatherSimulation:
         n = ctypes.c_int32()
         check(lib.ws_sim_steps_per_launch(self._h, ctypes.byref(n)))
         return n.value
+
+    def slab_schedule(self):
+        """Extension: (steps per halo exchange, overlap schedule on) of a slab (ws_hip.h
+        ws_sim_slab_schedule; (1, False) for a whole domain)."""
+        b, o = ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_sim_slab_schedule(self._h, ctypes.byref(b), ctypes.byref(o)))
+        return b.value, bool(o.value)
 
     def set_numerics(self, mode):
         """Extension: "exact" (bit-for-bit with the reference) or "fast" (FMA re-association,

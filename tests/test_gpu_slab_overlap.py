@@ -1,0 +1,165 @@
+"""The slab overlap schedule (ws_runtime.cpp overlap_block; north_star: the halo exchange
+overlapped with interior-cell compute on a second HIP stream): each block's edge bands run
+on the slab's edge stream and the exchange follows them there, while the interior rows run
+on the compute stream. It must equal the single-domain run bit-for-bit -- and so the
+stream-ordered deep-halo schedule -- for every kernel, integrator, block size, launch width
+and slab height, including slabs too thin for an interior (the edge bands merge and cover
+the whole slab) and runs ending mid-block.
+
+The group (one process, device-copy transport on its own stream between the slabs' edge
+streams) runs exactly the per-rank code (overlap_begin / overlap_edges / overlap_interior);
+the one-rank RCCL slab runs overlap_block itself with its no-op exchanges.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ws = pytest.importorskip("weather_sim")
+if not ws.is_cuda_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from weather_sim import _native  # noqa: E402
+
+
+def _cfg(W, H, method, fp64, L=1, model=0):
+    c = ws.SimulationConfig()
+    c.grid_width, c.grid_height, c.num_levels = W, H, L
+    c.model = model
+    c.integration_method, c.double_precision = method, fp64
+    c.dx, c.dy, c.coriolis_f = 1.0, 2.0, 0.25
+    return c
+
+
+def _pair(cfg_fn, nslabs, ic):
+    one = ws.WeatherSimulation(cfg_fn())
+    one.set_initial_condition(ic)
+    one.initialize()
+    group = ws.SlabGroup(cfg_fn(), nslabs)
+    group.set_initial_condition(ic)
+    group.initialize()
+    return one, group
+
+
+def _check(one, group, names=("u", "v", "h", "vorticity", "divergence")):
+    g1 = one.get_current_grid()
+    for name in names:
+        np.testing.assert_array_equal(group.gather(name), g1._get(name), err_msg=name)
+    assert group.slab(group.nslabs - 1).get_current_time() == one.get_current_time()
+
+
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "2"), ("lds", "1")])
+@pytest.mark.parametrize("block", ["1", "2", "3", "6"])
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_overlap_group_matches_single_domain(method, block, kernel, tb, monkeypatch):
+    """4 uneven slabs of 58-59 rows (room for an interior at every block size up to RK4 x 3),
+    fp64, runs of 13 and 2 steps (blocks + a partial block; a second run starts afresh)."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
+    monkeypatch.setenv("WS_SLAB_BLOCK", block)
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", tb)
+    monkeypatch.setenv("WS_SEG_ROWS", "16")
+    one, group = _pair(lambda: _cfg(170, 235, method, True), 4, ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
+    b, ovl = group.slab(1).slab_schedule()
+    assert ovl and b == min(int(block), 6)
+    for n in (13, 2):
+        assert group.run(n) == n
+        one.run(n)
+    _check(one, group)
+
+
+@pytest.mark.parametrize("nslabs", [2, 3, 5, 8])
+@pytest.mark.parametrize("fp64", [False, True])
+def test_overlap_thin_slabs_merge_bands(nslabs, fp64, monkeypatch):
+    """Forced overlap on slabs thinner than 2D (RK4, block 6: D = 24 rows): the edge bands
+    merge, the interior is empty, the edges carry the whole block."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
+    monkeypatch.setenv("WS_KERNEL", "dppy")
+    monkeypatch.setenv("WS_TB", "2")
+    one, group = _pair(lambda: _cfg(140, 8 * 21 + 3, 2, fp64), nslabs, ws.VortexInitialCondition())
+    assert group.slab(0).slab_schedule()[1]
+    for n in (7, 6):
+        assert group.run(n) == n
+        one.run(n)
+    _check(one, group)
+
+
+def test_overlap_is_default_for_deep_slabs(monkeypatch):
+    """Without WS_SLAB_OVERLAP: on when the thinnest slab holds 32 x block x NST rows (C2 at
+    4 GPUs: 1024 rows; off at 8: 512 < 768)."""
+    monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
+    monkeypatch.delenv("WS_SLAB_BLOCK", raising=False)
+    deep = ws.SlabGroup(_cfg(64, 4 * 1024, 2, True), 4)
+    thin = ws.SlabGroup(_cfg(64, 8 * 512, 2, True), 8)
+    assert deep.slab(0).slab_schedule() == (6, True)
+    assert thin.slab(0).slab_schedule() == (6, False)
+    assert ws.WeatherSimulation(_cfg(64, 64, 2, True)).slab_schedule() == (1, False)
+
+
+def test_overlap_pe_levels(monkeypatch):
+    """PE (3 levels, T / P drift on the aux stream, RK4 -> RK2) over 3 slabs with the overlap
+    schedule == one domain, every field."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
+    monkeypatch.setenv("WS_SLAB_BLOCK", "4")
+    one, group = _pair(lambda: _cfg(130, 150, 2, False, L=3, model=int(ws.SimulationModel.PrimitiveEquations)),
+                       3, ws.FrontInitialCondition())
+    for n in (9, 3):
+        assert group.run(n) == n
+        one.run(n)
+    _check(one, group, ("u", "v", "h", "t", "p", "q"))
+
+
+def test_overlap_default_autotuned(monkeypatch):
+    """The default configuration (autotuned kernel and launch width, no schedule knobs) on
+    slabs deep enough for the overlap schedule: on by default, == one domain."""
+    for k in ("WS_SLAB_OVERLAP", "WS_SLAB_BLOCK", "WS_KERNEL", "WS_TB", "WS_SEG_ROWS"):
+        monkeypatch.delenv(k, raising=False)
+    one, group = _pair(lambda: _cfg(256, 3 * 800, 2, True), 3, ws.JetStreamInitialCondition())
+    assert group.slab(2).slab_schedule() == (6, True)
+    assert group.run(12) == 12
+    one.run(12)
+    _check(one, group)
+
+
+def _uid():
+    buf = (ctypes.c_uint8 * _native.COMM_ID_BYTES)()
+    _native.check(_native.lib.ws_comm_get_unique_id(buf))
+    return bytes(buf)
+
+
+@pytest.mark.parametrize("method", [0, 2])
+def test_one_rank_rccl_slab_overlap(method, monkeypatch):
+    """overlap_block itself (the RCCL-mode function: exchange on the compute stream at the
+    first block, behind the edge bands on the edge stream afterwards) on a one-rank
+    communicator == one domain."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
+    one = ws.WeatherSimulation(_cfg(200, 61, method, True))
+    one.set_initial_condition(ws.VortexInitialCondition())
+    one.initialize()
+    slab = ws.WeatherSimulation(_cfg(200, 61, method, True), _slab=(0, 1, _uid()))
+    assert slab.slab_schedule() == (1, True)
+    slab.set_initial_condition(ws.VortexInitialCondition())
+    slab.initialize()
+    for n in (9, 4):
+        one.run(n)
+        slab.run(n)
+    for name in ("u", "v", "h", "vorticity", "divergence"):
+        np.testing.assert_array_equal(slab.get_current_grid()._get(name), one.get_current_grid()._get(name),
+                                      err_msg=name)
+
+
+@pytest.mark.parametrize("ovl", ["0", "1"])
+def test_emulated_slab_measurement_aid(ovl, monkeypatch):
+    """A slab without a communicator (tools/rank_timing.py): both schedules run, with the
+    pack / unpack kernels and the emulated transfer wait, and stay finite."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", ovl)
+    monkeypatch.setenv("WS_EMU_XFER_US", "5")
+    sim = ws.WeatherSimulation(_cfg(256, 4 * 100, 2, True), _slab=(1, 4, None))
+    assert (sim.row0, sim.rows) == (100, 100)
+    assert sim.slab_schedule() == (6, ovl == "1")
+    sim.set_initial_condition(ws.JetStreamInitialCondition())
+    sim.initialize()
+    assert sim.run(13) == 13
+    assert np.isfinite(sim.get_current_grid()._get("h")).all()
