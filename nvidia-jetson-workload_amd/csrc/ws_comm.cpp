@@ -47,12 +47,25 @@ void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const G
     if (nranks_ == 1) return;
     if (nfields > kMaxHaloFields) throw CommError("too many fields for one exchange");
     const HaloPlan plan = make_halo_plan(g, elem_size, rank_, nranks_, nfields, depth);
+    const ncclComm_t c = (ncclComm_t)comm_;
+    if (halo_direct(plan)) {
+        // the plan executed literally: one send / receive per (field, level) segment, posted
+        // in plan order (per neighbour: sends, then receives, field-major) on every rank, so
+        // the k-th send to a peer meets that peer's k-th receive from us
+        check(ncclGroupStart(), "ncclGroupStart");
+        for (const HaloXfer& x : plan.xfers()) {
+            char* p = (char*)fields[x.field] + x.offset;
+            if (x.kind == 0) check(ncclSend(p, (size_t)x.bytes, ncclChar, x.peer, c, stream), "ncclSend");
+            else check(ncclRecv(p, (size_t)x.bytes, ncclChar, x.peer, c, stream), "ncclRecv");
+        }
+        check(ncclGroupEnd(), "ncclGroupEnd");
+        return;
+    }
     staging_.ensure(plan.msg_bytes());
     HaloFields hf{};
     for (int f = 0; f < nfields; ++f) hf.f[f] = (char*)fields[f];
     for (int side = 0; side < 2; ++side)
         if (plan.has[side]) hcheck(halo_pack(plan, hf, side, staging_.send[side], stream), "halo_pack");
-    const ncclComm_t c = (ncclComm_t)comm_;
     const size_t bytes = (size_t)plan.msg_bytes();
     check(ncclGroupStart(), "ncclGroupStart");
     for (int side = 0; side < 2; ++side) {

@@ -51,6 +51,13 @@ struct HaloPlan {
 
 HaloPlan make_halo_plan(const Geom& g, int elem_size, int rank, int nranks, int nfields, int depth);
 
+// Transport choice: with few segments per neighbour (SWE: 3 fields x 1 level) each segment
+// moves by its own send / receive straight between the field rows (no pack / unpack
+// kernels on the exchange's critical path); with many (PE: 3 x L levels) they are packed
+// into one message per neighbour.
+constexpr int kDirectSegs = 4;
+inline bool halo_direct(const HaloPlan& p) { return p.nfields * p.L <= kDirectSegs; }
+
 struct HaloFields {
     char* f[kMaxHaloFields];
 };

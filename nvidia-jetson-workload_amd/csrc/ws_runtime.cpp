@@ -520,6 +520,10 @@ void slab_exchange(ws_sim* s, ws_grid* g, int nfields, int depth, hipStream_t st
     }
     if (s->nranks < 2 || s->emu_xfer_us < 0 || s->in_group) return;
     const ws::HaloPlan plan = ws::make_halo_plan(g->geom(), (int)elem_size(s->dtype), s->rank, s->nranks, nfields, depth);
+    if (ws::halo_direct(plan)) {  // direct sends (ws_comm.cpp): the transfer only
+        WS_HIP_CHECK(ws::emulated_transfer(s->emu_xfer_us, st));
+        return;
+    }
     if (!s->staging) s->staging = new ws::HaloStaging;
     s->staging->ensure(plan.msg_bytes());
     ws::HaloFields hf{};
@@ -1910,10 +1914,30 @@ void group_exchange(ws_group* gr, int nfields, int depth, bool next = false, hip
     const int n = (int)gr->slabs.size();
     std::vector<ws::HaloPlan> plans(n);
     std::vector<ws::HaloFields> hf(n);
+    auto grid = [&](int r) { ws_sim* s = gr->slabs[r]; return s->slot[next ? 1 - s->cur : s->cur]; };
+    for (int r = 0; r < n; ++r) {
+        const ws_grid* me = grid(r);
+        plans[r] = ws::make_halo_plan(me->geom(), (int)elem_size(me->dtype), r, n, nfields, depth);
+    }
+    if (ws::halo_direct(plans[0])) {
+        // the direct transport (ws_comm.cpp): every send segment of the plan lands on the
+        // receive segment the peer's plan lists for it (same field / level, the k-th of each)
+        for (int r = 0; r < n; ++r)
+            for (const ws::HaloXfer& x : plans[r].xfers()) {
+                if (x.kind != 0) continue;
+                for (const ws::HaloXfer& y : plans[x.peer].xfers())
+                    if (y.kind == 1 && y.peer == r && y.field == x.field && y.level == x.level) {
+                        require(y.bytes == x.bytes, WS_ERR_COMM, "halo segment size mismatch");
+                        WS_HIP_CHECK(hipMemcpyAsync((char*)grid(x.peer)->f[y.field] + y.offset,
+                                                    (const char*)grid(r)->f[x.field] + x.offset, (size_t)x.bytes,
+                                                    hipMemcpyDeviceToDevice, st));
+                    }
+            }
+        return;
+    }
     for (int r = 0; r < n; ++r) {
         ws_sim* s = gr->slabs[r];
-        const ws_grid* me = s->slot[next ? 1 - s->cur : s->cur];
-        plans[r] = ws::make_halo_plan(me->geom(), (int)elem_size(me->dtype), r, n, nfields, depth);
+        const ws_grid* me = grid(r);
         if (!s->staging) s->staging = new ws::HaloStaging;
         s->staging->ensure(plans[r].msg_bytes());
         for (int f = 0; f < nfields; ++f) hf[r].f[f] = (char*)me->f[f];

@@ -90,11 +90,33 @@ class SlabBuffers:
         return self.buf[f].view(np.uint8)
 
 
+K_DIRECT_SEGS = 4  # ws_halo.h kDirectSegs
+
+
 def execute_plan(slab, plan):
     """Run one exchange of the library's plan over gloo, as SlabComm::exchange does over RCCL:
-    pack the send segments into one message per peer (msg_offset order), send / receive,
-    unpack into the receive segments."""
+    with at most kDirectSegs segments per neighbour (SWE), one send / receive per segment
+    straight from / into the field rows, posted in plan order; else pack the send segments
+    into one message per peer (msg_offset order), send / receive, unpack into the receive
+    segments."""
     peers = sorted({x.peer for x in plan})
+    if all(sum(1 for x in plan if x.peer == p and x.kind == 0) <= K_DIRECT_SEGS for p in peers):
+        reqs, landing = [], []
+        for x in plan:
+            buf = slab.bytes_of(x.field)
+            o = slab.row0_bytes + x.offset
+            assert 0 <= o and o + x.bytes <= buf.size
+            if x.kind == 0:
+                reqs.append(dist.isend(torch.from_numpy(buf[o:o + x.bytes].copy()), x.peer))
+            else:
+                t = torch.zeros(x.bytes, dtype=torch.uint8)
+                reqs.append(dist.irecv(t, x.peer))
+                landing.append((buf, o, t))
+        for r in reqs:
+            r.wait()
+        for buf, o, t in landing:
+            buf[o:o + t.numel()] = t.numpy()
+        return
     msg_len = {p: max(x.msg_offset + x.bytes for x in plan if x.peer == p and x.kind == 0) for p in peers}
     for p in peers:  # the receive message has the send message's shape
         assert msg_len[p] == max(x.msg_offset + x.bytes for x in plan if x.peer == p and x.kind == 1)
