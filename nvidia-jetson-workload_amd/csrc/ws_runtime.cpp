@@ -1132,12 +1132,13 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             const int thin = cfg->grid_height / slab.nranks;
             s->block = std::max(1, std::min(6, std::min(ws::kHalo, thin) / nst));
             if (const char* e = std::getenv("WS_SLAB_BLOCK")) s->block = std::max(1, std::min(s->block, std::atoi(e)));
-            // overlap schedule (overlap_block) when the slabs are deep: its edge bands cost ~11 %
-            // more stencil work plus two cross-stream waits per block, which the hidden
-            // exchange repays at C2's 4 slabs (1024 rows: 0.044 -> 0.039 ms/step with a 40 us
-            // transfer) but not surely at 8 (512 rows: break-even near 60-80 us per exchange;
-            // tools/rank_timing.py). Every rank decides alike (global quantities).
-            s->overlap = thin >= 32 * s->block * nst;
+            // overlap schedule (overlap_block) when the slabs have an interior beside the two
+            // edge bands: its edge bands cost ~11 % more stencil work plus two cross-stream
+            // waits per block, which the hidden exchange repays from ~2 / 20 / 35 us per
+            // exchange at C2's 2 / 4 / 8 slabs (tools/rank_timing.py; a 2.4 MB
+            // message per neighbour over one xGMI link is ~40-55 us). Every rank decides
+            // alike (global quantities only).
+            s->overlap = thin >= 3 * s->block * nst;
             if (const char* e = std::getenv("WS_SLAB_OVERLAP")) s->overlap = std::atoi(e) != 0;
         } else if (comm && s->fused) {
             s->overlap = env_int("WS_SLAB_OVERLAP", 0) != 0;

@@ -87,12 +87,12 @@ def test_overlap_thin_slabs_merge_bands(nslabs, fp64, monkeypatch):
 
 
 def test_overlap_is_default_for_deep_slabs(monkeypatch):
-    """Without WS_SLAB_OVERLAP: on when the thinnest slab holds 32 x block x NST rows (C2 at
-    4 GPUs: 1024 rows; off at 8: 512 < 768)."""
+    """Without WS_SLAB_OVERLAP: on when the thinnest slab holds 3 x block x NST rows (C2 at 8
+    GPUs: 512 >= 72), off below."""
     monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
     monkeypatch.delenv("WS_SLAB_BLOCK", raising=False)
-    deep = ws.SlabGroup(_cfg(64, 4 * 1024, 2, True), 4)
-    thin = ws.SlabGroup(_cfg(64, 8 * 512, 2, True), 8)
+    deep = ws.SlabGroup(_cfg(64, 8 * 512, 2, True), 8)
+    thin = ws.SlabGroup(_cfg(64, 4 * 40, 2, True), 4)
     assert deep.slab(0).slab_schedule() == (6, True)
     assert thin.slab(0).slab_schedule() == (6, False)
     assert ws.WeatherSimulation(_cfg(64, 64, 2, True)).slab_schedule() == (1, False)
@@ -116,7 +116,7 @@ def test_overlap_default_autotuned(monkeypatch):
     slabs deep enough for the overlap schedule: on by default, == one domain."""
     for k in ("WS_SLAB_OVERLAP", "WS_SLAB_BLOCK", "WS_KERNEL", "WS_TB", "WS_SEG_ROWS"):
         monkeypatch.delenv(k, raising=False)
-    one, group = _pair(lambda: _cfg(256, 3 * 800, 2, True), 3, ws.JetStreamInitialCondition())
+    one, group = _pair(lambda: _cfg(256, 3 * 100, 2, True), 3, ws.JetStreamInitialCondition())
     assert group.slab(2).slab_schedule() == (6, True)
     assert group.run(12) == 12
     one.run(12)
