@@ -416,6 +416,7 @@ def main():
     stats = sim.kernel_timing()
     variant, seg_rows, out_cols = sim.fused_variant()
     tb = sim.steps_per_launch()
+    block, overlap = sim.slab_schedule()
     dev_ms, launches = sim.last_run_stats()
     # dominant kernel = largest total device time
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
@@ -441,7 +442,10 @@ def main():
         "data": "synthetic (reference jet_stream/zonal_flow initial condition), inputs resident in HBM",
         "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [conf["W"], conf["H"]],
                    "levels": conf["L"], "integrator": args.method,
-                   "parallelism": f"y-slab x{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"y-slab x{world}" if world > 1 else "single GPU",
+                   **({"slab_schedule": {"steps_per_exchange": block,
+                                         "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap]}}
+                      if world > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
