@@ -13,9 +13,11 @@ for f in ws_runtime.cpp ws_initial_conditions.cpp ws_comm.cpp; do
 done
 wait
 HIPOBJ=$(ls _obj/*.hip.o)
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -shared-libasan -fsanitize=address,undefined -o "$OUT/libws_hip_san.so" \
-    "$OUT"/*.cpp.o $HIPOBJ -L/opt/rocm/lib -lrccl -lhipfft -Wl,-rpath,/opt/rocm/lib
 CLANG=/opt/rocm/lib/llvm/bin/clang
+# Host-only link with plain clang++ (the device code objects are already embedded in the
+# .o files): the sanitizer runtime is a host library, nothing here targets the GPU.
+${CLANG}++ -shared -shared-libasan -fsanitize=address,undefined -o "$OUT/libws_hip_san.so" \
+    "$OUT"/*.cpp.o $HIPOBJ -L/opt/rocm/lib -lamdhip64 -lrccl -lhipfft -Wl,-rpath,/opt/rocm/lib
 $CLANG -g -O1 -fsanitize=address,undefined -fno-sanitize-recover=all -shared-libasan -I../../include \
     ../../tools/sanitize/abi_host_check.c -o "$OUT/abi_host_check" -L"$OUT" -lws_hip_san -Wl,-rpath,"$OUT" \
     -Wl,-rpath,$(dirname $($CLANG -print-file-name=libclang_rt.asan-x86_64.so))
