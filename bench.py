@@ -162,6 +162,107 @@ def cpu_baseline(conf, method, budget_s=20.0):
                       f"OMP_NUM_THREADS={threads} ({how})"}
 
 
+SLAB_GOLDEN = os.path.join(ROOT, "tests", "golden", "ref_slab_digests.json")
+FAST_TOL = 1e-10  # north_star: fields within 1e-10 relative L2 of the reference (fp64)
+
+
+def load_slab_golden():
+    """Reference per-slab digests (tests/golden/gen_slab_digests.py): C2 jet_stream RK4 fp64."""
+    if not os.path.exists(SLAB_GOLDEN):
+        return None
+    with open(SLAB_GOLDEN) as f:
+        return json.load(f)
+
+
+def slab_sha256(fields):
+    import hashlib
+    import numpy as np
+    return {k: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() for k, a in fields.items()}
+
+
+def verdict_over_ranks(dist, ok):
+    """Every rank learns whether all ranks passed (MIN over a gloo group; world 1: itself)."""
+    if dist is None or not dist.is_initialized():
+        return bool(ok)
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t[0])
+
+
+def sum_over_ranks(dist, values):
+    if dist is None or not dist.is_initialized():
+        return list(values)
+    import torch
+    t = torch.tensor(list(values), dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
+
+
+def check_slab_parity(dist, rank, world, row0, rows, exact_fields, fast_fields, golden):
+    """The self-check of a (multi-GPU) run against the reference, before the timed region.
+
+    exact_fields: this rank's owned rows of u, v, h, vorticity after golden["steps"] steps in
+    exact numerics -- their SHA-256 must equal the reference's for this rank of this world
+    size (bit-for-bit, every rank). fast_fields (or None): the same run in the fp64 default
+    fast numerics -- relative L2 against the exact (= reference) fields over the whole grid
+    (sums over ranks) must be <= FAST_TOL. Returns (verdict "ok" | "fail", detail dict); every
+    rank returns the same verdict."""
+    import numpy as np
+    want = golden["slabs"].get(str(world))
+    detail = {"case": golden["case"], "steps": golden["steps"], "ranks_checked": world}
+    if want is None:
+        detail["error"] = f"no reference digests for {world} ranks"
+        return "fail", detail
+    mine = want[rank]
+    ok = mine["row0"] == row0 and mine["rows"] == rows
+    got = slab_sha256(exact_fields)
+    bad = sorted(k for k in golden["fields"] if got.get(k) != mine["sha256"][k])
+    ok = ok and not bad
+    exact_ok = verdict_over_ranks(dist, ok)
+    detail["exact"] = "bitwise == reference" if exact_ok else "MISMATCH"
+    if not ok:
+        detail["rank_mismatch"] = {"rank": rank, "fields": bad, "row0": row0, "rows": rows}
+    fast_ok = True
+    if fast_fields is not None:
+        sums = []
+        for k in ("u", "v", "h"):
+            e = exact_fields[k].astype(np.float64)
+            d = fast_fields[k].astype(np.float64) - e
+            sums += [float(np.sum(d * d)), float(np.sum(e * e))]
+        tot = sum_over_ranks(dist, sums)
+        rel = {k: (tot[2 * i] ** 0.5) / max(tot[2 * i + 1] ** 0.5, 1e-300) for i, k in enumerate(("u", "v", "h"))}
+        detail["fast_rel_l2"] = rel
+        detail["fast_tol"] = FAST_TOL
+        fast_ok = all(np.isfinite(v) and v <= FAST_TOL for v in rel.values())
+    return ("ok" if exact_ok and fast_ok else "fail"), detail
+
+
+def slab_fields(sim):
+    g = sim.get_current_grid()
+    u, v = g.get_velocity_field()
+    return {"u": u, "v": v, "h": g.get_height_field(), "vort": g.get_vorticity_field()}
+
+
+def self_check(sim, ic, dist, rank, world, golden):
+    """Run the golden case on this simulation (exact, then the default numerics) and check it."""
+    default = sim.get_numerics()
+    sim.set_numerics("exact")
+    sim.set_initial_condition(ic)
+    sim.initialize()
+    assert sim.run(golden["steps"]) == golden["steps"]
+    exact = slab_fields(sim)
+    fast = None
+    if default != "exact":
+        sim.set_numerics(default)
+        sim.initialize()
+        assert sim.run(golden["steps"]) == golden["steps"]
+        fast = slab_fields(sim)
+    row0 = getattr(sim, "row0", 0) or 0
+    rows = exact["u"].shape[0]
+    return check_slab_parity(dist, rank, world, row0, rows, exact, fast, golden)
+
+
 def bvort_words_per_cell(method, W, H):
     """Algorithmic traffic of one barotropic step in words per cell: per RK stage an R2C
     (read W*H reals, write (W/2+1)*H complex), the column pass (read + write the spectrum;
@@ -347,6 +448,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--method", default="rk4", choices=sorted(METHODS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the parity self-check (profiling runs)")
     args = ap.parse_args()
 
     os.environ.setdefault("WS_QUIET", "1")
@@ -386,6 +488,15 @@ def main():
         sim = ws.WeatherSimulation(cfg)
 
     ic = {"jet_stream": ws.JetStreamInitialCondition, "zonal_flow": ws.ZonalFlowInitialCondition}[conf["ic"]]()
+    # parity self-check before the timed region: the reference's per-slab digests of the C2
+    # jet_stream RK4 fp64 case (bitwise, exact numerics) and the default numerics within the
+    # north_star tolerance; a failure is reported and the run exits non-zero
+    parity, parity_detail = None, {"note": "self-check covers the c2 rk4 workload"}
+    golden = load_slab_golden()
+    if args.config == "c2" and args.method == "rk4" and golden is not None and not args.no_check:
+        parity, parity_detail = self_check(sim, ic, dist if world > 1 else None, rank, world, golden)
+        if rank == 0:
+            log(f"parity self-check: {parity} {json.dumps(parity_detail)}")
     sim.set_initial_condition(ic)
     sim.initialize()  # on a slab, the IC is evaluated in global coordinates for the owned rows
 
@@ -475,10 +586,14 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             log(f"cpu baseline failed: {e!r}")
             result["cpu_baseline"] = None
+    result["parity"] = parity
+    result["parity_detail"] = parity_detail
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity == "fail":
+        sys.exit(3)
 
 
 if __name__ == "__main__":
