@@ -592,7 +592,7 @@ int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
             ws::hck(hipMalloc(&b->ax, (size_t)nk * b->es()), "hipMalloc");
             ws::hck(hipMalloc(&b->ay, (size_t)b->H * b->es()), "hipMalloc");
             for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc})
-                ws::hck(hipMemset(p, 0, fb), "hipMemset");
+                ws::hck(hipMemsetAsync(p, 0, fb, b->stream), "hipMemsetAsync");  // ordered with the model's stream
             const bool f64 = b->dtype == WS_F64;
             auto pow2 = [](int n) { return n >= 16 && n <= 4096 && (n & (n - 1)) == 0; };
             const char* fe = std::getenv("WS_BV_FFT");

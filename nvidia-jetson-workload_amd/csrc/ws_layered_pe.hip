@@ -370,7 +370,7 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
             for (int s = 0; s < 2; ++s)
                 for (void*& p : m->S[s]) {
                     ws::hck(hipMalloc(&p, fb), "hipMalloc");
-                    ws::hck(hipMemset(p, 0, fb), "hipMemset");
+                    ws::hck(hipMemsetAsync(p, 0, fb, m->stream), "hipMemsetAsync");  // ordered with the model's stream
                 }
             for (void** grp : {m->A, m->B, m->acc})
                 for (int i = 0; i < 3; ++i) ws::hck(hipMalloc(&grp[i], fb), "hipMalloc");

@@ -141,7 +141,10 @@ void grid_alloc(ws_grid* g, unsigned nfields) {
     const size_t stagger = (size_t)env_int("WS_FIELD_STAGGER", 0) / 256 * 256;  // bytes, field i offset by i*stagger
     for (unsigned i = 0; i < nfields; ++i) {
         WS_HIP_CHECK(hipMalloc(&g->alloc[i], g->bytes_per_field() + i * stagger));
-        WS_HIP_CHECK(hipMemset(g->alloc[i], 0, g->bytes_per_field() + i * stagger));
+        // on the grid's own stream: a legacy-stream hipMemset is not ordered with the
+        // non-blocking streams the kernels run on, and returns before it completes -- it raced
+        // with the first launches writing a freshly allocated overlap grid (slab groups)
+        WS_HIP_CHECK(hipMemsetAsync(g->alloc[i], 0, g->bytes_per_field() + i * stagger, g->stream));
         g->f[i] = (char*)g->alloc[i] + i * stagger + (size_t)ws::kHalo * g->pitch * es;
     }
 }

@@ -58,3 +58,19 @@ def test_bench_self_check_one_domain(monkeypatch):
     assert max(detail["fast_rel_l2"].values()) <= 1e-10
     assert 0 < max(detail["fast_rel_l2"].values())  # fast numerics really ran
     assert sim.get_numerics() == "fast"
+
+
+def test_fresh_overlap_groups_repeatable(monkeypatch):
+    """Regression: the overlap grids of a slab are allocated at the first overlapped run; their
+    zeroing once ran as a legacy-stream hipMemset, unordered with the (non-blocking) slab
+    streams, and raced with the first edge-band launches (seam 0/1 wrong in ~1 of 4 fresh
+    4-slab groups). Fresh groups, run at once, several times."""
+    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
+    for _ in range(4):
+        group = ws.SlabGroup(_cfg(), 4)
+        group.set_initial_condition(ws.JetStreamInitialCondition())
+        group.initialize()
+        assert group.run(GOLD["steps"]) == GOLD["steps"]
+        for r in range(4):
+            assert bench.slab_sha256(bench.slab_fields(group.slab(r))) == GOLD["slabs"]["4"][r]["sha256"], f"slab {r}"
+        del group
