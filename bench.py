@@ -449,6 +449,8 @@ def main():
     ap.add_argument("--method", default="rk4", choices=sorted(METHODS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the parity self-check (profiling runs)")
+    ap.add_argument("--pin", default=None, help="kernel:steps_per_launch:seg_rows:align (profiling runs pin "
+                                                "the variant a bench run chose)")
     args = ap.parse_args()
 
     os.environ.setdefault("WS_QUIET", "1")
@@ -487,6 +489,9 @@ def main():
     else:
         sim = ws.WeatherSimulation(cfg)
 
+    if args.pin:
+        k, tb, seg, al = args.pin.split(":")
+        sim.pin_variant(kernel=k, steps_per_launch=int(tb), seg_rows=int(seg) or None, align=bool(int(al)))
     ic = {"jet_stream": ws.JetStreamInitialCondition, "zonal_flow": ws.ZonalFlowInitialCondition}[conf["ic"]]()
     # parity self-check before the timed region: the reference's per-slab digests of the C2
     # jet_stream RK4 fp64 case (bitwise, exact numerics) and the default numerics within the

@@ -23,6 +23,17 @@
  *   ws_device_info / ws_is_available AdaptiveKernelManager::getDeviceCapabilities / isCudaAvailable
  *                                                            include/weather_sim/gpu_adaptability.hpp:128-237
  *   ws_comm_* / ws_sim_create_slab   (new: the reference has no distributed path)
+ *
+ * Environment switches read by the library (all optional; everything else is an argument):
+ *   WS_NUMERICS=exact|fast    numerics of the fused kernels at creation (ws_sim_set_numerics)
+ *   WS_FUSED=0                per-stage kernels instead of the fused step kernel
+ *   WS_KERNEL=x2y|dppy|lds    pin the fused-kernel variant      } each also settable per
+ *   WS_TB=1|2                 pin the steps per fused launch    } simulation with
+ *   WS_SEG_ROWS=n             pin the rows per kernel segment   } ws_sim_pin_variant
+ *   WS_AUTOTUNE=0|1|2         variant autotuner off / on (default) / on + print its table
+ *   WS_TUNE_CACHE=path        append / reuse autotune choices across processes
+ *   WS_SLAB_OVERLAP=0|1       fix the slab overlap schedule (default: chosen from a measured
+ *                             halo exchange, ws_sim_set_slab_schedule)
  */
 #ifndef WS_HIP_H
 #define WS_HIP_H
@@ -34,7 +45,7 @@
 extern "C" {
 #endif
 
-#define WS_ABI_VERSION 1
+#define WS_ABI_VERSION 2
 
 /* status codes */
 enum {
@@ -211,13 +222,18 @@ int ws_launch_diagnostics_kernels(const void* d_u, const void* d_v, void* d_vort
 int ws_comm_get_unique_id(uint8_t id[WS_COMM_ID_BYTES]);
 /* One rank of a y-slab decomposition of the global grid described by cfg. Rank r owns
  * rows [row0, row0 + rows) (balanced split, returned); halo rows are exchanged with
- * ncclSend/ncclRecv between neighbouring ranks. Fields set / read through the slab's
- * grids are the local rows only. Results are bitwise identical to one GPU.
- * id == NULL (measurement aid): the slab gets no communicator -- its halo exchanges are
- * skipped and the halo rows keep what they hold -- so one process can time one rank's
- * compute schedule of an N-rank decomposition on one GPU (results then differ). */
+ * ncclSend/ncclRecv between neighbouring ranks (id: from ws_comm_get_unique_id on one rank,
+ * the same bytes on every rank; NULL is an error). Fields set / read through the slab's
+ * grids are the local rows only. Results are bitwise identical to one GPU. */
 int ws_sim_create_slab(const ws_config_t* cfg, int32_t rank, int32_t nranks, const uint8_t id[WS_COMM_ID_BYTES],
                        ws_sim_t** out, int32_t* row0, int32_t* rows);
+/* Measurement aid: rank `rank`'s slab WITHOUT a communicator. Its halo exchanges are
+ * replaced by a device-side wait of xfer_us microseconds (the direct transport) or the
+ * pack / unpack kernels around that wait (the packed one), so one process can time one
+ * rank's whole schedule of an N-rank decomposition on one GPU; the halo rows keep what they
+ * hold, so results differ from the decomposed run (timing only). nranks >= 2. */
+int ws_sim_create_slab_emulated(const ws_config_t* cfg, int32_t rank, int32_t nranks, double xfer_us,
+                                ws_sim_t** out, int32_t* row0, int32_t* rows);
 
 /* Slab group: the same y-slab decomposition and step schedule (interior segments while the
  * halo moves, then edge segments) inside ONE process on one device, halo rows moved by
@@ -236,7 +252,10 @@ int ws_group_run(ws_group_t* group, int32_t num_steps, int32_t* steps_taken);
  * level). Per neighbour there is ONE message: its send segments (kind 0) concatenated in
  * plan order (field-major, then level; msg_offset = position in the message), received
  * into the receive segments (kind 1) in the same order. ws_sim_create_slab's RCCL exchange
- * and ws_group_run's device copies both execute exactly this plan (pack, move, unpack).
+ * and ws_group_run's device copies both execute exactly this plan: with at most 4 segments
+ * per neighbour (SWE: u, v, h) every segment moves by its own send / receive straight
+ * between the field rows (the direct transport); with more (PE: 3 x levels) they are packed
+ * into the one message, moved and unpacked.
  * out = NULL: only count / pitch / level_stride. */
 typedef struct {
     int32_t peer;        /* neighbour rank */
@@ -269,6 +288,11 @@ int ws_sim_comm_barrier(ws_sim_t* sim);
  * Euler), double_precision and device_id. */
 typedef struct ws_bvort ws_bvort_t;
 int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out);
+/* poisson: WS_POISSON_AUTO = the LDS-resident FFT passes on power-of-two grids up to 4096,
+ * hipFFT's 2-D plans otherwise; WS_POISSON_HIPFFT = hipFFT always (cross-check). */
+#define WS_POISSON_AUTO 0
+#define WS_POISSON_HIPFFT 1
+int ws_bvort_create_poisson(const ws_config_t* cfg, int32_t poisson, ws_bvort_t** out);
 int ws_bvort_destroy(ws_bvort_t* model);
 /* (height, width) C-contiguous host array, fp32 or fp64 (converted like a C cast) */
 int ws_bvort_set_vorticity(ws_bvort_t* model, const void* host, int32_t height, int32_t width, int32_t dtype);
@@ -321,10 +345,19 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
  * kernels (ids 1-3 are retired variants); seg_rows = output rows per segment, out_cols =
  * output columns per strip (a multiple of the 128-byte line when the strips are
  * line-aligned). Chosen by timing every variant on the real grid at the first run (all give
- * identical results), unless WS_KERNEL / WS_SEG_ROWS / WS_ALIGN fix it. The choice is
- * cached per process by (grid shape, levels, precision, integrator, numerics, slab
- * position), and a slab decomposition uses rank 0's choice on every rank. */
+ * identical results), unless WS_KERNEL / WS_SEG_ROWS / ws_sim_pin_variant fix it. The
+ * choice is cached per process by (grid shape, levels, precision, model, integrator,
+ * numerics, slab position and block), and a slab decomposition uses rank 0's choice on every
+ * rank. */
 int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols);
+
+/* Pin (part of) the fused-kernel variant of one simulation; -1 leaves a part to the
+ * autotuner. kernel: WS_KERNEL_LDS / _DPPY / _X2Y; steps_per_launch: 1 or 2; seg_rows:
+ * output rows per segment; align: 1 = strip output windows on whole 128-byte lines. */
+#define WS_KERNEL_LDS 0
+#define WS_KERNEL_DPPY 4
+#define WS_KERNEL_X2Y 5
+int ws_sim_pin_variant(ws_sim_t* sim, int32_t kernel, int32_t steps_per_launch, int32_t seg_rows, int32_t align);
 
 /* Time steps per fused launch the simulation's run() uses where it can (new; temporal
  * blocking): 1, or 2 = the dppy kernel advances two steps per launch (y_n read once,
@@ -337,9 +370,19 @@ int ws_sim_steps_per_launch(const ws_sim_t* sim, int32_t* steps);
  * exchange (deep halo of block x NST rows; 1 for a whole domain), overlap = 1 when run()
  * uses the overlap schedule -- each block's edge bands (the rows the neighbours need) on a
  * second HIP stream followed there by the halo exchange, the interior rows meanwhile on the
- * compute stream (bit-identical to the stream-ordered schedule). Default: overlap when the
- * thinnest slab has at least 3 x block x NST rows; WS_SLAB_OVERLAP=0|1 fixes it. */
+ * compute stream (bit-identical to the stream-ordered schedule).
+ * Default (WS_OVERLAP_AUTO): at the first run rank 0 times the block's halo exchange on the
+ * real communicator and every rank runs the overlap schedule iff that exchange takes longer
+ * than the edge bands' measured cost (needs >= 3 x block x NST rows per slab); a slab group
+ * (one process) overlaps whenever there is an interior. WS_SLAB_OVERLAP=0|1 fixes it.
+ * ws_sim_set_slab_schedule: block (> 0; <= 0 keeps it; every rank must pass the same values)
+ * and overlap mode; ws_sim_slab_exchange_us: the measured exchange (auto mode; -1 if none). */
+#define WS_OVERLAP_OFF 0
+#define WS_OVERLAP_ON 1
+#define WS_OVERLAP_AUTO 2
 int ws_sim_slab_schedule(const ws_sim_t* sim, int32_t* block, int32_t* overlap);
+int ws_sim_set_slab_schedule(ws_sim_t* sim, int32_t block, int32_t overlap);
+int ws_sim_slab_exchange_us(const ws_sim_t* sim, double* us);
 
 /* CFL number of the current state (new: the reference's dt is fixed and it has no CFL):
  * max over cells of max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy), computed in

@@ -397,7 +397,7 @@ struct ws_bvort {
     void* z[2] = {nullptr, nullptr};
     void *A = nullptr, *B = nullptr, *psi = nullptr, *acc = nullptr, *spec = nullptr, *ax = nullptr, *ay = nullptr;
     void *u = nullptr, *v = nullptr;
-    // LDS-FFT Poisson path (power-of-two W, H; WS_BV_FFT=hipfft selects the library)
+    // LDS-FFT Poisson path (power-of-two W, H; WS_POISSON_HIPFFT at creation selects the library)
     bool lds_fft = false;
     void *twW = nullptr, *twH = nullptr;
     int logw = 0, logh = 0, cw = 1;
@@ -562,7 +562,9 @@ using ws::AbiError;
 
 extern "C" {
 
-int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
+int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) { return ws_bvort_create_poisson(cfg, WS_POISSON_AUTO, out); }
+
+int ws_bvort_create_poisson(const ws_config_t* cfg, int32_t poisson, ws_bvort_t** out) {
     return ws::abi_guarded([&] {
         if (!cfg || !out) throw AbiError(WS_ERR_INVALID, "null argument");
         if (cfg->grid_width < 3 || cfg->grid_height < 3)
@@ -595,14 +597,14 @@ int ws_bvort_create(const ws_config_t* cfg, ws_bvort_t** out) {
                 ws::hck(hipMemsetAsync(p, 0, fb, b->stream), "hipMemsetAsync");  // ordered with the model's stream
             const bool f64 = b->dtype == WS_F64;
             auto pow2 = [](int n) { return n >= 16 && n <= 4096 && (n & (n - 1)) == 0; };
-            const char* fe = std::getenv("WS_BV_FFT");
-            b->lds_fft = pow2(b->W) && pow2(b->H) && !(fe && std::strcmp(fe, "hipfft") == 0);
+            if (poisson != WS_POISSON_AUTO && poisson != WS_POISSON_HIPFFT) throw AbiError(WS_ERR_INVALID, "bad poisson mode");
+            b->lds_fft = pow2(b->W) && pow2(b->H) && poisson != WS_POISSON_HIPFFT;
             if (b->lds_fft) {
                 while ((1 << b->logw) < b->W) ++b->logw;
                 while ((1 << b->logh) < b->H) ++b->logh;
-                // adjacent spectrum columns per column-pass workgroup: <= 64 KB of LDS
-                const char* cwe = std::getenv("WS_BV_CW");
-                const size_t col_budget = cwe ? (size_t)std::atoi(cwe) * b->H * 2 * b->es() : 65536;
+                // adjacent spectrum columns per column-pass workgroup: <= 64 KB of LDS (1 / 2 / 8
+                // columns measured no better than the 4 this gives at 2048^2 fp32)
+                const size_t col_budget = 65536;
                 while (b->cw < 16 && (size_t)2 * b->cw * b->H * 2 * b->es() <= col_budget) b->cw *= 2;
                 // at most kColPer elements per thread of the column pass
                 while (b->cw > 1 && (size_t)b->cw * b->H > (size_t)(f64 ? 512 : 1024) * ws::kColPer) b->cw /= 2;

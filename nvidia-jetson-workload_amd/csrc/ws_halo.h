@@ -67,7 +67,7 @@ hipError_t halo_pack(const HaloPlan& p, const HaloFields& fields, int side, void
 // scatter a received message into side `side`'s halo rows of `fields`
 hipError_t halo_unpack(const HaloPlan& p, const HaloFields& fields, int side, const void* src, hipStream_t s);
 
-// Measurement aid (a slab without a communicator, WS_EMU_XFER_US): one workgroup that
+// Measurement aid (a slab without a communicator, ws_sim_create_slab_emulated): one workgroup that
 // holds the stream for `us` microseconds of wall clock -- the place of the transfer in the
 // schedule, without the transfer.
 hipError_t emulated_transfer(double us, hipStream_t s);

@@ -266,11 +266,8 @@ template <typename T>
 void stage(ws_lpe* m, void* const* in, void* const* out, T c, T w, int acc_mode) {
     LpeArgs<T> a{};
     const int ti = tot_index(m, in), to = tot_index(m, out);
-    static const bool carry = [] {
-        const char* e = std::getenv("WS_LPE_TOTALS");  // 0: every stage sums the thickness itself
-        return !(e && std::atoi(e) == 0);
-    }();
-    a.tin = carry && m->tot_ok[ti] ? (const T*)m->tot[ti] : nullptr;
+    // the input's total thickness when the producing stage wrote it (else the scan sums it)
+    a.tin = m->tot_ok[ti] ? (const T*)m->tot[ti] : nullptr;
     a.tout = (T*)m->tot[to];
     m->tot_ok[to] = true;
     a.u = (const T*)in[0];

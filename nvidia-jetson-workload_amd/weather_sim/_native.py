@@ -113,6 +113,10 @@ SIGNATURES = {
     "ws_launch_diagnostics_kernels": [_P, _P, _P, _P, _I, _I, ctypes.c_int64, _D, _D, _I, _P],
     "ws_comm_get_unique_id": [ctypes.POINTER(ctypes.c_uint8)],
     "ws_sim_create_slab": [ctypes.POINTER(ws_config_t), _I, _I, ctypes.POINTER(ctypes.c_uint8), _PP, _PI, _PI],
+    "ws_sim_create_slab_emulated": [ctypes.POINTER(ws_config_t), _I, _I, _D, _PP, _PI, _PI],
+    "ws_sim_set_slab_schedule": [_P, _I, _I],
+    "ws_sim_slab_exchange_us": [_P, _PD],
+    "ws_sim_pin_variant": [_P, _I, _I, _I, _I],
     "ws_slab_partition": [_I, _I, _I, _PI, _PI],
     "ws_sim_comm_allreduce_max": [_P, _D, _PD],
     "ws_sim_comm_barrier": [_P],
@@ -130,6 +134,7 @@ SIGNATURES = {
     "ws_sim_get_numerics": [_P, _PI],
     "ws_slab_exchange_plan": [_I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ws_xfer_t), _I, _PI, _PL, _PL],
     "ws_bvort_create": [ctypes.POINTER(ws_config_t), _PP],
+    "ws_bvort_create_poisson": [ctypes.POINTER(ws_config_t), _I, _PP],
     "ws_bvort_destroy": [_P],
     "ws_bvort_set_vorticity": [_P, _P, _I, _I, _I],
     "ws_bvort_get_field": [_P, _I, _P, _I, _I, _I],

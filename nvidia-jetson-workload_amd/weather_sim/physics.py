@@ -31,14 +31,20 @@ _FIELDS = {"vorticity": 0, "streamfunction": 1, "u": 2, "v": 3}
 class BarotropicVorticityModel:
     """One barotropic vorticity model on the device (no CPU path: fails without a GPU)."""
 
-    def __init__(self, config):
+    _POISSON = {"auto": 0, "hipfft": 1}
+
+    def __init__(self, config, poisson="auto"):
+        """poisson: "auto" (LDS-resident FFT passes on power-of-two grids up to 4096, hipFFT
+        otherwise) or "hipfft" (hipFFT's 2-D plans always; ws_hip.h ws_bvort_create_poisson)."""
         from .weather_simulation import SimulationConfig
         if not isinstance(config, SimulationConfig):
             raise TypeError("BarotropicVorticityModel expects a SimulationConfig")
+        if poisson not in self._POISSON:
+            raise ValueError(f"poisson must be one of {sorted(self._POISSON)}")
         self._cfg = config
         raw = config._to_c()
         h = ctypes.c_void_p()
-        check(lib.ws_bvort_create(ctypes.byref(raw), ctypes.byref(h)))
+        check(lib.ws_bvort_create_poisson(ctypes.byref(raw), self._POISSON[poisson], ctypes.byref(h)))
         self._h = h
         self.width, self.height = int(config.grid_width), int(config.grid_height)
         self.dtype = np.float64 if config.double_precision else np.float32

@@ -532,12 +532,18 @@ class WeatherSimulation:
         if _slab is None:
             check(lib.ws_sim_create(ctypes.byref(c), ctypes.byref(h)))
         else:
-            rank, nranks, uid = _slab
+            # (rank, nranks, uid): one rank's slab over RCCL; (rank, nranks, None, xfer_us): the
+            # communicator-less measurement slab (ws_hip.h ws_sim_create_slab_emulated)
+            rank, nranks, uid = _slab[:3]
             r0, nr = ctypes.c_int32(), ctypes.c_int32()
-            # uid None: no communicator (measurement aid, ws_hip.h ws_sim_create_slab)
-            idbuf = None if uid is None else (ctypes.c_uint8 * _native.COMM_ID_BYTES).from_buffer_copy(uid)
-            check(lib.ws_sim_create_slab(ctypes.byref(c), int(rank), int(nranks), idbuf, ctypes.byref(h),
-                                         ctypes.byref(r0), ctypes.byref(nr)))
+            if uid is None:
+                xfer_us = float(_slab[3]) if len(_slab) > 3 else 0.0
+                check(lib.ws_sim_create_slab_emulated(ctypes.byref(c), int(rank), int(nranks), xfer_us,
+                                                      ctypes.byref(h), ctypes.byref(r0), ctypes.byref(nr)))
+            else:
+                idbuf = (ctypes.c_uint8 * _native.COMM_ID_BYTES).from_buffer_copy(uid)
+                check(lib.ws_sim_create_slab(ctypes.byref(c), int(rank), int(nranks), idbuf, ctypes.byref(h),
+                                             ctypes.byref(r0), ctypes.byref(nr)))
             self.row0, self.rows = r0.value, nr.value
         self._h = h
         _say(f"Using compute backend: {_BACKEND_NAMES.get(int(config.compute_backend), 'HIP GPU (MI355X)')}")
@@ -706,6 +712,29 @@ class WeatherSimulation:
         check(lib.ws_sim_slab_schedule(self._h, ctypes.byref(b), ctypes.byref(o)))
         return b.value, bool(o.value)
 
+    _OVERLAP = {"off": 0, "on": 1, "auto": 2, False: 0, True: 1}
+    _KERNELS = {"lds": 0, "dppy": 4, "x2y": 5}
+
+    def set_slab_schedule(self, block=0, overlap="auto"):
+        """Extension: steps per halo exchange (block > 0; 0 keeps it) and the overlap schedule
+        ("off" / "on" / "auto": chosen from a measured exchange; ws_hip.h
+        ws_sim_set_slab_schedule). Every rank of a decomposition must pass the same values."""
+        check(lib.ws_sim_set_slab_schedule(self._h, int(block), self._OVERLAP[overlap]))
+
+    def slab_exchange_us(self):
+        """Extension: the halo exchange time the auto schedule measured (-1: not measured)."""
+        us = ctypes.c_double()
+        check(lib.ws_sim_slab_exchange_us(self._h, ctypes.byref(us)))
+        return us.value
+
+    def pin_variant(self, kernel=None, steps_per_launch=None, seg_rows=None, align=None):
+        """Extension: fix (parts of) the fused-kernel variant the autotuner would choose
+        (ws_hip.h ws_sim_pin_variant); None leaves a part to the autotuner."""
+        check(lib.ws_sim_pin_variant(self._h, -1 if kernel is None else self._KERNELS[kernel],
+                                     -1 if steps_per_launch is None else int(steps_per_launch),
+                                     -1 if seg_rows is None else int(seg_rows),
+                                     -1 if align is None else int(bool(align))))
+
     def set_numerics(self, mode):
         """Extension: "exact" (bit-for-bit with the reference) or "fast" (FMA re-association,
         the fp64 default; ws_hip.h WS_NUMERICS_*) for the fused step kernels."""
@@ -752,6 +781,15 @@ class SlabGroup:
 
     def slab(self, rank):
         return self._slabs[rank]
+
+    def set_slab_schedule(self, block=0, overlap="auto"):
+        """Every slab's block and overlap schedule (WeatherSimulation.set_slab_schedule)."""
+        for s in self._slabs:
+            s.set_slab_schedule(block, overlap)
+
+    def pin_variant(self, **kw):
+        for s in self._slabs:
+            s.pin_variant(**kw)
 
     def set_initial_condition(self, ic):
         self._ic = ic

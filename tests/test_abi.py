@@ -78,7 +78,7 @@ def test_config_default_matches_reference_defaults():
 
 
 def test_abi_version_and_availability():
-    assert _native.lib.ws_abi_version() == 1
+    assert _native.lib.ws_abi_version() == 2
     assert isinstance(_native.is_available(), bool)
 
 
@@ -150,3 +150,20 @@ def test_api_surface_mirrors_reference():
     assert [m.value for m in ws.IntegrationMethod] == [0, 1, 2, 3, 4]
     info = ws.get_device_info()
     assert "cuda_available" in info and "device_name" in info
+
+
+def test_environment_switches_are_few_and_documented():
+    """The library reads at most 8 WS_* environment variables, each listed in ws_hip.h (the
+    rest of the configuration is ABI arguments: ws_sim_pin_variant, ws_sim_set_slab_schedule,
+    ws_sim_create_slab_emulated, ws_bvort_create_poisson)."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = set()
+    for f in glob.glob(os.path.join(root, "nvidia-jetson-workload_amd", "csrc", "*")):
+        if f.endswith((".cpp", ".hip", ".h")):
+            names |= set(re.findall(r'(?:getenv|env_str|env_int)\("(WS_[A-Z0-9_]+)"', open(f).read()))
+    header = open(os.path.join(root, "include", "ws_hip.h")).read()
+    assert 0 < len(names) <= 8, sorted(names)
+    for n in names:
+        assert f" *   {n}=" in header, n

@@ -10,14 +10,14 @@ from oracle import bvort_oracle as bo
 pytestmark = pytest.mark.gpu
 
 
-def model(W, H, method=2, fp64=True, dx=1.0, dy=1.0, dt=0.05, beta=0.0, nu=0.0):
+def model(W, H, method=2, fp64=True, dx=1.0, dy=1.0, dt=0.05, beta=0.0, nu=0.0, poisson="auto"):
     import weather_sim as ws
     c = ws.SimulationConfig()
     c.grid_width, c.grid_height = W, H
     c.integration_method = method
     c.double_precision = fp64
     c.dx, c.dy, c.dt, c.beta, c.viscosity = dx, dy, dt, beta, nu
-    return ws.BarotropicVorticityModel(c)
+    return ws.BarotropicVorticityModel(c, poisson=poisson)
 
 
 def smooth_field(W, H, seed=0):
@@ -113,16 +113,14 @@ def test_errors():
 @pytest.mark.parametrize("fft", ["lds", "hipfft"])
 def test_poisson_paths_fp64(W, H, fft, monkeypatch):
     """Power-of-two grids take the three-pass LDS FFT Poisson solve (ws_bvort.hip
-    bv_rowfft_fwd / bv_colsolve / bv_rowfft_inv); WS_BV_FFT=hipfft the library's 2-D plans.
+    bv_rowfft_fwd / bv_colsolve / bv_rowfft_inv); poisson="hipfft" the library's 2-D plans.
     Both against the oracle's pocketfft solve and three RK4 steps. On the strongly
     anisotropic grids (aspect 256) the Jacobian's derivatives along the long axis amplify
     the FFTs' round-off (either FFT; ~3e-9 relative after three steps), hence 1e-8 there."""
-    if fft == "hipfft":
-        monkeypatch.setenv("WS_BV_FFT", "hipfft")
     # the smooth field's streamfunction (and so its velocity) grows with the grid: keep the
     # advective CFL number below ~0.5
     kw = dict(dx=1.0, dy=1.25, dt=0.05 * min(1.0, 64.0 / max(W, H)), beta=0.3, nu=0.02)
-    m = model(W, H, 2, True, **kw)
+    m = model(W, H, 2, True, poisson="auto" if fft == "lds" else "hipfft", **kw)
     z0 = smooth_field(W, H, seed=W + 3 * H)
     z0 -= z0.mean()
     m.set_vorticity(z0)

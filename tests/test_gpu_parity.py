@@ -268,13 +268,12 @@ def test_full_size_digests(name, tb, monkeypatch):
                         f"|ref|={ref_l2!r})")
 
 
-@pytest.mark.parametrize("aux,tb", [("1", "0"), ("0", "0"), ("1", "2")])
-def test_pe_levels_match_reference_per_level(aux, tb, monkeypatch):
+@pytest.mark.parametrize("tb", ["0", "2"])
+def test_pe_levels_match_reference_per_level(tb, monkeypatch):
     """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
-    must equal a standalone reference run of that level (bitwise) -- with the T / P update
-    on the second stream (WS_PE_AUX=1, the default) and on the main stream, and with two
-    steps per launch (dppy, two T / P updates per launch)."""
-    monkeypatch.setenv("WS_PE_AUX", aux)
+    must equal a standalone reference run of that level (bitwise) -- the T / P update on
+    the second stream, with the autotuned kernel and with two steps per launch (dppy, two
+    T / P updates per launch)."""
     if tb != "0":
         monkeypatch.setenv("WS_KERNEL", "dppy")
         monkeypatch.setenv("WS_TB", tb)

@@ -56,12 +56,11 @@ def _check(one, group, names=("u", "v", "h", "vorticity", "divergence")):
 def test_overlap_group_matches_single_domain(method, block, kernel, tb, monkeypatch):
     """4 uneven slabs of 58-59 rows (room for an interior at every block size up to RK4 x 3),
     fp64, runs of 13 and 2 steps (blocks + a partial block; a second run starts afresh)."""
-    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
-    monkeypatch.setenv("WS_SLAB_BLOCK", block)
     monkeypatch.setenv("WS_KERNEL", kernel)
     monkeypatch.setenv("WS_TB", tb)
     monkeypatch.setenv("WS_SEG_ROWS", "16")
     one, group = _pair(lambda: _cfg(170, 235, method, True), 4, ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
+    group.set_slab_schedule(int(block), "on")
     b, ovl = group.slab(1).slab_schedule()
     assert ovl and b == min(int(block), 6)
     for n in (13, 2):
@@ -87,10 +86,9 @@ def test_overlap_thin_slabs_merge_bands(nslabs, fp64, monkeypatch):
 
 
 def test_overlap_is_default_for_deep_slabs(monkeypatch):
-    """Without WS_SLAB_OVERLAP: on when the thinnest slab holds 3 x block x NST rows (C2 at 8
-    GPUs: 512 >= 72), off below."""
+    """Without WS_SLAB_OVERLAP a slab group (no transfer to measure) overlaps when the
+    thinnest slab holds 3 x block x NST rows (C2 at 8 GPUs: 512 >= 72), not below."""
     monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
-    monkeypatch.delenv("WS_SLAB_BLOCK", raising=False)
     deep = ws.SlabGroup(_cfg(64, 8 * 512, 2, True), 8)
     thin = ws.SlabGroup(_cfg(64, 4 * 40, 2, True), 4)
     assert deep.slab(0).slab_schedule() == (6, True)
@@ -101,10 +99,9 @@ def test_overlap_is_default_for_deep_slabs(monkeypatch):
 def test_overlap_pe_levels(monkeypatch):
     """PE (3 levels, T / P drift on the aux stream, RK4 -> RK2) over 3 slabs with the overlap
     schedule == one domain, every field."""
-    monkeypatch.setenv("WS_SLAB_OVERLAP", "1")
-    monkeypatch.setenv("WS_SLAB_BLOCK", "4")
     one, group = _pair(lambda: _cfg(130, 150, 2, False, L=3, model=int(ws.SimulationModel.PrimitiveEquations)),
                        3, ws.FrontInitialCondition())
+    group.set_slab_schedule(4, "on")
     for n in (9, 3):
         assert group.run(n) == n
         one.run(n)
@@ -114,7 +111,7 @@ def test_overlap_pe_levels(monkeypatch):
 def test_overlap_default_autotuned(monkeypatch):
     """The default configuration (autotuned kernel and launch width, no schedule knobs) on
     slabs deep enough for the overlap schedule: on by default, == one domain."""
-    for k in ("WS_SLAB_OVERLAP", "WS_SLAB_BLOCK", "WS_KERNEL", "WS_TB", "WS_SEG_ROWS"):
+    for k in ("WS_SLAB_OVERLAP", "WS_KERNEL", "WS_TB", "WS_SEG_ROWS"):
         monkeypatch.delenv(k, raising=False)
     one, group = _pair(lambda: _cfg(256, 3 * 100, 2, True), 3, ws.JetStreamInitialCondition())
     assert group.slab(2).slab_schedule() == (6, True)
@@ -152,14 +149,44 @@ def test_one_rank_rccl_slab_overlap(method, monkeypatch):
 
 @pytest.mark.parametrize("ovl", ["0", "1"])
 def test_emulated_slab_measurement_aid(ovl, monkeypatch):
-    """A slab without a communicator (tools/rank_timing.py): both schedules run, with the
-    pack / unpack kernels and the emulated transfer wait, and stay finite."""
+    """A slab without a communicator (ws_sim_create_slab_emulated, tools/rank_timing.py):
+    both schedules run, with the emulated transfer wait, and stay finite."""
     monkeypatch.setenv("WS_SLAB_OVERLAP", ovl)
-    monkeypatch.setenv("WS_EMU_XFER_US", "5")
-    sim = ws.WeatherSimulation(_cfg(256, 4 * 100, 2, True), _slab=(1, 4, None))
+    sim = ws.WeatherSimulation(_cfg(256, 4 * 100, 2, True), _slab=(1, 4, None, 5.0))
     assert (sim.row0, sim.rows) == (100, 100)
     assert sim.slab_schedule() == (6, ovl == "1")
     sim.set_initial_condition(ws.JetStreamInitialCondition())
     sim.initialize()
     assert sim.run(13) == 13
     assert np.isfinite(sim.get_current_grid()._get("h")).all()
+
+
+@pytest.mark.parametrize("xfer_us,expect", [(0.0, False), (150.0, True)])
+def test_auto_schedule_from_measured_exchange(xfer_us, expect, monkeypatch):
+    """WS_OVERLAP_AUTO (the multi-GPU default): the first run times the block's halo exchange
+    and overlaps only when it costs more than the edge bands' break-even (~35 us at slabs of
+    a few hundred rows). On the emulated slab the exchange is a timed wait of xfer_us."""
+    monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
+    sim = ws.WeatherSimulation(_cfg(256, 4 * 100, 2, True), _slab=(1, 4, None, xfer_us))
+    assert sim.slab_exchange_us() == -1.0 and sim.slab_schedule() == (6, False)  # not measured yet
+    sim.set_initial_condition(ws.JetStreamInitialCondition())
+    sim.initialize()
+    assert sim.run(7) == 7
+    us = sim.slab_exchange_us()
+    assert us >= xfer_us * 0.9 and us < xfer_us + 1000.0
+    assert sim.slab_schedule() == (6, expect)
+    sim.set_slab_schedule(3, "off")  # fixed by the caller from now on
+    assert sim.slab_schedule() == (3, False) and sim.slab_exchange_us() == -1.0
+    assert sim.run(4) == 4
+    with pytest.raises(ValueError):
+        sim.set_slab_schedule(7, "on")  # 7 x 4 rows > the 24 halo rows
+
+
+def test_create_slab_requires_an_id():
+    """ws_sim_create_slab no longer accepts a NULL id (a caller bug would silently skip every
+    halo exchange); the measurement slab has its own entry point."""
+    c = _cfg(64, 64, 2, True)
+    h, r0, nr = ctypes.c_void_p(), ctypes.c_int32(), ctypes.c_int32()
+    st = _native.lib.ws_sim_create_slab(ctypes.byref(c._to_c()), 0, 2, None, ctypes.byref(h), ctypes.byref(r0),
+                                        ctypes.byref(nr))
+    assert st != 0 and "null communicator id" in _native.lib.ws_last_error().decode()

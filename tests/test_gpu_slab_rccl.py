@@ -58,7 +58,6 @@ def test_slab_blocks_are_bitwise(block, kernel, method, monkeypatch):
     """Slabs advance `block` steps per halo exchange (block x NST halo rows, steps computed
     on rows extended into the halo): 4 slabs == one domain bit-for-bit for every block
     size, kernel and integrator, over a run that ends mid-block."""
-    monkeypatch.setenv("WS_SLAB_BLOCK", block)
     monkeypatch.setenv("WS_KERNEL", kernel)
 
     def cfg():
@@ -73,6 +72,7 @@ def test_slab_blocks_are_bitwise(block, kernel, method, monkeypatch):
     one.set_initial_condition(ic)
     one.initialize()
     group = ws.SlabGroup(cfg(), 4)
+    group.set_slab_schedule(int(block), "off")
     group.set_initial_condition(ic)
     group.initialize()
     for n in (7, 2):  # 7 = two blocks of 3 + one step; a second run starts a new block

@@ -11,7 +11,7 @@ if not ws.is_cuda_available():  # pragma: no cover
     pytest.skip("no HIP device", allow_module_level=True)
 
 
-def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3):
+def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3, align=None):
     from oracle.ws_oracle import OracleSim
 
     c = ws.SimulationConfig()
@@ -19,6 +19,8 @@ def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3):
     c.integration_method, c.double_precision = method, fp64
     c.dx, c.dy, c.coriolis_f = dx, dy, f
     sim = ws.WeatherSimulation(c)
+    if align is not None:
+        sim.pin_variant(align=align)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
     sim.initialize()
     g = sim.get_current_grid()
@@ -63,9 +65,9 @@ def test_non_pow2_spacing(kernel, tb, method, monkeypatch):
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_line_aligned_strips(W, kernel, tb, method, fp64, monkeypatch):
-    """WS_ALIGN=1: strip output windows cut to whole 128-byte lines (asymmetric margins)."""
+    """align=1 (ws_sim_pin_variant): strip output windows cut to whole 128-byte lines
+    (asymmetric margins)."""
     monkeypatch.setenv("WS_KERNEL", kernel)
     monkeypatch.setenv("WS_TB", tb)
-    monkeypatch.setenv("WS_ALIGN", "1")
     monkeypatch.setenv("WS_SEG_ROWS", "9")
-    run_both(W, 37, method, fp64, 5)
+    run_both(W, 37, method, fp64, 5, align=True)

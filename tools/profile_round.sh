@@ -22,18 +22,18 @@ g=16//(8 if '$CFG' in ('c2','c5') or '$CFG'.startswith('c2_') else 4)
 margin=(cone+g-1)//g*g if k in ('dppy','x2y') else cone
 full={'dppy':64,'x2y':128,'lds':256}[k]-2*margin
 print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0, tb)")
-echo "pinned: WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN WS_TB=$TB"
-export WS_KERNEL=$KERN WS_SEG_ROWS=$SEG WS_ALIGN=$ALIGN WS_TB=$TB
+PIN="$KERN:$TB:$SEG:$ALIGN"
+echo "pinned: --pin $PIN (kernel:steps per launch:seg rows:align)"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+    python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline --no-check --pin $PIN > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
-      python3 "$R/bench.py" --config $CFG --method $METHOD --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/pmc/p$i.log" 2>&1
+      python3 "$R/bench.py" --config $CFG --method $METHOD --steps 20 --warmup 2 --no-cpu-baseline --no-check --pin $PIN > "$OUT/pmc/p$i.log" 2>&1
   rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc/p$i.log"; exit $rc; }
 done
 python3 "$R/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc_summary.txt"

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """One rank's step time in an N-rank y-slab decomposition, on ONE GPU (measurement aid).
 
-Creates rank r's slab of the global grid WITHOUT a communicator (ws_sim_create_slab with a
-NULL id): its run() executes the rank's exact compute schedule -- deep-halo blocks, stream-
-ordered or overlapped (WS_SLAB_OVERLAP) -- with the halo pack / unpack kernels around a
-wall-clock wait of WS_EMU_XFER_US microseconds in place of each RCCL transfer. Results are
+Creates rank r's slab of the global grid WITHOUT a communicator (ws_sim_create_slab_emulated):
+its run() executes the rank's exact compute schedule -- deep-halo blocks, stream-ordered or
+overlapped (set_slab_schedule) -- with a device-side wait of the given microseconds in place
+of each RCCL transfer (around the pack / unpack kernels for the packed transport). Results are
 not a simulation (the halo holds the slab's own rows); the time per step is what an
 N-GPU rank would spend if the transfer took that long.
   python tools/rank_timing.py [--config c2] [--ranks 2,4,8] [--xfer-us 0,30,60]
@@ -31,7 +31,7 @@ ap.add_argument("--xfer-us", default="0,30,60", help="per exchange of a 6-step b
                 "plus --xfer-lat-us for other block sizes")
 ap.add_argument("--xfer-lat-us", type=float, default=10.0)
 ap.add_argument("--blocks", default="6")
-ap.add_argument("--variants", default="0,1", help="WS_SLAB_OVERLAP values")
+ap.add_argument("--variants", default="off,on", help="overlap schedules: off, on, auto")
 args = ap.parse_args()
 conf = bench.CONFIGS[args.config]
 
@@ -42,19 +42,17 @@ for n in [int(x) for x in args.ranks.split(",")]:
             us = 0.0 if us6 == 0 else args.xfer_lat_us + (us6 - args.xfer_lat_us) * int(blk) / 6
             line = []
             for var in args.variants.split(","):
-                os.environ["WS_SLAB_OVERLAP"] = var
-                os.environ["WS_SLAB_BLOCK"] = blk
-                os.environ["WS_EMU_XFER_US"] = str(us)
                 c = ws.SimulationConfig()
                 c.grid_width, c.grid_height, c.num_levels = conf["W"], conf["H"], conf["L"]
                 c.model, c.integration_method = conf["model"], bench.METHODS[args.method]
                 c.double_precision = conf["fp64"]
                 c.max_time = 1e30
-                sim = ws.WeatherSimulation(c, _slab=(rank, n, None))
+                sim = ws.WeatherSimulation(c, _slab=(rank, n, None, us))
+                sim.set_slab_schedule(int(blk), var)
                 sim.set_initial_condition(ws.JetStreamInitialCondition())
                 sim.initialize()
+                sim.run(300)  # autotune (+ the auto schedule's measurement) + warm clocks
                 block, on = sim.slab_schedule()
-                sim.run(300)  # autotune + warm clocks
                 best = None
                 for _ in range(3):
                     t0 = time.perf_counter()

@@ -80,6 +80,15 @@ static int check_no_device_paths(void) {
         return 27;
     double d = 0;
     if (ws_sim_cfl(NULL, &d, NULL, 0, NULL) != WS_ERR_INVALID) return 28;
+    ws_config_default(&cfg);
+    int32_t r0 = 0, nr = 0;
+    /* a NULL communicator id is an error (the measurement slab has its own entry point) */
+    if (ws_sim_create_slab(&cfg, 0, 2, NULL, &sim, &r0, &nr) != WS_ERR_INVALID) return 29;
+    if (ws_sim_create_slab_emulated(&cfg, 0, 1, 5.0, &sim, &r0, &nr) != WS_ERR_INVALID) return 30;
+    if (ws_sim_create_slab_emulated(&cfg, 0, 2, -1.0, &sim, &r0, &nr) != WS_ERR_INVALID) return 31;
+    if (ws_sim_pin_variant(NULL, -1, -1, -1, -1) != WS_ERR_INVALID) return 32;
+    if (ws_sim_set_slab_schedule(NULL, 6, WS_OVERLAP_AUTO) != WS_ERR_INVALID) return 33;
+    if (ws_bvort_create_poisson(&cfg, 7, NULL) != WS_ERR_INVALID) return 34;
     return 0;
 }
 

@@ -8,7 +8,7 @@ OUT=${OUT:-/tmp/ws_host_sanitize}
 mkdir -p "$OUT"
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer"
 FLAGS="-O1 -g -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-result -I../../include -I/opt/rocm/include"
-for f in ws_runtime.cpp ws_initial_conditions.cpp ws_comm.cpp; do
+for f in ws_runtime.cpp ws_schedule.cpp ws_autotune.cpp ws_slab.cpp ws_initial_conditions.cpp ws_comm.cpp; do
   /opt/rocm/bin/hipcc $FLAGS $SAN -x hip -c $f -o "$OUT/$f.o" &
 done
 wait

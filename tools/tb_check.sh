@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU: parity suite, then the C2 autotune table (WS_TUNE_LOG=1) and a bench line per config.
+# GPU: parity suite, then the C2 autotune table (WS_AUTOTUNE=2) and a bench line per config.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/tb; mkdir -p $OUT
@@ -9,7 +9,7 @@ if [ "${TESTS:-1}" = "1" ]; then
 fi
 for spec in ${CFGS:-c2:rk4}; do
   c=${spec%%:*}; m=${spec##*:}
-  WS_TUNE_LOG=1 timeout -k 10 300 python bench.py --config $c --method $m --steps ${STEPS:-200} --warmup ${WARM:-300} --no-cpu-baseline > $OUT/${c}_$m.json 2> $OUT/${c}_$m.err
+  WS_AUTOTUNE=2 timeout -k 10 300 python bench.py --config $c --method $m --steps ${STEPS:-200} --warmup ${WARM:-300} --no-cpu-baseline > $OUT/${c}_$m.json 2> $OUT/${c}_$m.err
   rc=$?; [ $rc -eq 0 ] || { echo "$spec rc=$rc"; tail -5 $OUT/${c}_$m.err; exit $rc; }
   grep "autotune" $OUT/${c}_$m.err | sort -t' ' -k11 -n | head -8
   python3 -c "
