@@ -34,6 +34,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "cell-updates/sec + achieved HBM GB/s, SWE 4096^2 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
+VALU_CYCLES = 4        # a wave64 VALU instruction occupies its SIMD16 for 4 cycles (fp64 full rate)
+RAMP_S = 0.4           # untimed sustained load before the timed steps (DVFS clock ramp)
 
 CONFIGS = {
     "c2": dict(W=4096, H=4096, L=1, model=0, fp64=True, ic="jet_stream",
@@ -511,6 +515,13 @@ def main():
 
     if args.warmup > 0:
         sim.run(args.warmup)
+    # clock ramp (untimed): the chip raises its clocks over tens of milliseconds of sustained
+    # load, and W short warm-up steps from idle leave the timed steps on the ramp (measured:
+    # C2 0.243 ms per two-step launch warm vs 0.277 when the timed run starts cold). Keep the
+    # GPU busy for >= RAMP_S seconds of untimed steps first; reported as ramp_steps.
+    ramp_steps, t_ramp = 0, time.perf_counter()
+    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
+        ramp_steps += sim.run(20)
     sim.set_kernel_timing(True, reserve=4 * args.steps + 16)  # events created outside the timed region
     barrier()
     torch.cuda.synchronize()
@@ -538,11 +549,20 @@ def main():
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
     achieved = bpl / (tot_ms / n * 1e-3) / 1e9
     step_bytes = sum(b for (_, _, b) in stats.values()) / tb  # one launch per kind covers tb steps
-    traffic = None
+    # PMC of the same variant (tools/profile_round.sh -> profiles/traffic_<config>_<method>.json):
+    # HBM bytes and VALU wave-instructions per launch
+    traffic, valu_insts = None, None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
-    if os.path.exists(tfile):
+    if os.path.exists(tfile) and world == 1:
         with open(tfile) as f:
-            traffic = json.load(f).get(f"kind{kind}")
+            tj = json.load(f)
+        traffic, valu_insts = tj.get(f"kind{kind}"), tj.get("valu_insts")
+    launch_s = tot_ms / n * 1e-3
+    # compulsory bytes of one launch: y_n read + y_(n+k) written once (6 words per cell, the
+    # k steps in between never leave the chip)
+    compulsory = bpl / tb if variant != "stage_kernels" else bpl
+    valu_frac = valu_insts * VALU_CYCLES / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
+    dram_frac = traffic / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
     result = {
         "metric": METRIC,
         "value": value,
@@ -550,6 +570,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "ramp_steps": ramp_steps,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong",
@@ -560,10 +581,22 @@ def main():
                    "levels": conf["L"], "integrator": args.method,
                    "parallelism": f"y-slab x{world}" if world > 1 else "single GPU",
                    **({"slab_schedule": {"steps_per_exchange": block,
-                                         "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap]}}
+                                         "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap],
+                                         "measured_exchange_us": sim.slab_exchange_us(),
+                                         "choice": "auto: overlap iff the measured block exchange exceeds the edge "
+                                                   "bands' break-even (ws_autotune.cpp choose_slab_schedule)"
+                                                   if os.environ.get("WS_SLAB_OVERLAP") is None else
+                                                   "fixed by WS_SLAB_OVERLAP"}}
                       if world > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "frac_kind": "one-step-equivalent: the HBM rate a one-step-per-launch kernel would need "
+                                  "for this cell-update rate (6 words per cell-update); with two steps per "
+                                  "launch it can exceed 1 -- the measured utilisations are compulsory_frac, "
+                                  "dram_frac and valu_frac",
+                     "traffic": traffic,
+                     "compulsory_gbs": compulsory / launch_s / 1e9,
+                     "compulsory_frac": compulsory / launch_s / 1e9 / HBM_PEAK_GBS,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
                      "seg_rows": seg_rows, "strip_out_cols": out_cols, "steps_per_launch": tb,
                      "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n,
@@ -575,8 +608,14 @@ def main():
                                     f"and writes y_(n+2) once, so its traffic is about half its algorithmic bytes: "
                                     f"dram_gbs is the measured DRAM rate"
                                     if variant != "stage_kernels" else "SURVEY 8(d) stage-kernel words per launch"),
-                     "dram_gbs": traffic / (tot_ms / n * 1e-3) / 1e9 if traffic else None,
-                     "dram_frac": traffic / (tot_ms / n * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None},
+                     "dram_gbs": traffic / launch_s / 1e9 if traffic else None,
+                     "dram_frac": dram_frac,
+                     "valu_insts_per_launch": valu_insts,
+                     "valu_frac": valu_frac,
+                     "valu_model": f"SQ_INSTS_VALU (wave64 instructions per launch, PMC) x {VALU_CYCLES} cycles / "
+                                   f"({SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz x mean launch time)",
+                     "binding": (None if valu_frac is None or dram_frac is None
+                                 else "valu" if valu_frac > dram_frac else "hbm")},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
         "cfl": {"value": cfl, "reduction_ms": cfl_ms,
                 "gbs": 3 * (8 if conf["fp64"] else 4) * cells / world / (cfl_ms * 1e-3) / 1e9 if cfl_ms > 0 else None,

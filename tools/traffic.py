@@ -13,7 +13,8 @@ import os
 import sys
 
 root, sub, out = sys.argv[1], sys.argv[2], sys.argv[3]
-vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+vals = {"FETCH_SIZE": [], "WRITE_SIZE": [], "SQ_INSTS_VALU": [], "SQ_INSTS_LDS": [], "SQ_LDS_BANK_CONFLICT": [],
+        "GRBM_GUI_ACTIVE": []}
 for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for row in csv.DictReader(fh):
@@ -24,6 +25,12 @@ write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 res = {"kind0": 2 * fetch * 1024 + write * 1024, "fetch_size_kib_reported": fetch, "write_size_kib": write,
        "dispatches": [len(vals["FETCH_SIZE"]), len(vals["WRITE_SIZE"])], "kernel": sub,
        "correction": "bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024); gfx950 FETCH_SIZE halving"}
+mean = lambda k: sum(vals[k]) / len(vals[k]) if vals[k] else None  # noqa: E731
+res["valu_insts"] = mean("SQ_INSTS_VALU")
+res["lds_insts"] = mean("SQ_INSTS_LDS")
+res["lds_bank_conflict_cycles"] = mean("SQ_LDS_BANK_CONFLICT")
+res["grbm_gui_active"] = mean("GRBM_GUI_ACTIVE")
+res["dispatches"] += [len(vals["SQ_INSTS_VALU"])]
 with open(out, "w") as f:
     json.dump(res, f, indent=1)
 print(json.dumps(res))
