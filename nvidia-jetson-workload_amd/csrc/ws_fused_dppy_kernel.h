@@ -441,11 +441,19 @@ __global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Ge
 
 // Launch fused_dppy_kernel<T, nstages, NSTEP, mode, CPL> (one translation unit per (T,
 // NSTEP, CPL): ws_fused_dppy{,2}_<t>_<n>.hip, compiled in parallel).
+// measurement builds only (-DWS_DPPY_LDS_PAD=bytes): unused dynamic LDS per wave, capping the
+// waves per SIMD for occupancy A/B runs
+#ifdef WS_DPPY_LDS_PAD
+constexpr unsigned kLdsPad = WS_DPPY_LDS_PAD;
+#else
+constexpr unsigned kLdsPad = 0;
+#endif
+
 template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
     const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(kWave);
 #define WS_DPPY_GO(N, M) \
-    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL>), grid, block, 0, s, a, g, nstrips, nsegs)
+    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)
 #define WS_DPPY_G1(M) WS_DPPY_GO(1, M)
 #define WS_DPPY_G2(M) WS_DPPY_GO(2, M)
 #define WS_DPPY_G4(M) WS_DPPY_GO(4, M)
