@@ -301,6 +301,9 @@ def bench_bvort(args, conf, method, world):
     m.set_vorticity(z0)
     if args.warmup > 0:
         m.run(args.warmup)
+    t_ramp = time.perf_counter()  # clock ramp (untimed), as in main()
+    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
+        m.run(2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     m.run(args.steps)
@@ -397,6 +400,9 @@ def bench_lpe(args, conf, method, world):
     m.set_state(*s0)
     if args.warmup > 0:
         m.run(args.warmup)
+    t_ramp = time.perf_counter()  # clock ramp (untimed), as in main()
+    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
+        m.run(2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     m.run(args.steps)

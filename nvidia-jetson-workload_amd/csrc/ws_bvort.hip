@@ -152,10 +152,15 @@ struct Cx {
     T x, y;
 };
 
-// LDS index padding: one spare element per 16 breaks the power-of-two strides of the
-// bit-reversed scatter and the short-span passes out of a single bank group
-__device__ __forceinline__ int P(int i) { return i + (i >> 4); }
-__host__ __device__ constexpr size_t padded(size_t n) { return n + n / 16 + 1; }
+// LDS index swizzle: element i lives at slot i ^ (((i >> 3) ^ (i >> 4) ^ (i >> 9)) & 31) -- a
+// permutation inside each aligned block of 32 elements (256 B, every bank once for 8-byte
+// elements). Chosen by a GF(2) search over shift-xor maps (tools/lds_swizzle.py): every
+// 32-lane ds_read_b64 group of the FFT passes (radix-8 groups at strides 1 / 8 / 64..., the
+// bit-reversed row / column gathers, 4-column blocks at stride H) touches 32 distinct slots,
+// and every 16-lane ds_write_b64 group at most 2 per bank (modelled at 2048: 32 + 831 extra
+// LDS cycles where the round-2 "+1 per 16" padding had 6 912 + 9 920).
+__device__ __forceinline__ int P(int i) { return i ^ (((i >> 3) ^ (i >> 4) ^ (i >> 9)) & 31); }
+__host__ __device__ constexpr size_t padded(size_t n) { return (n + 31) / 32 * 32; }
 
 __device__ __forceinline__ int bitrev(int i, int logn) { return (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - logn)); }
 
@@ -415,6 +420,7 @@ namespace ws {
 namespace {
 
 void bv_free(ws_bvort* b) {
+    if (b->stream) (void)hipStreamSynchronize(b->stream);  // nothing queued may touch freed memory
     for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay, b->u, b->v, b->twW, b->twH})
         if (p) (void)hipFree(p);
     if (b->have_r2c) hipfftDestroy(b->r2c);
@@ -594,7 +600,10 @@ int ws_bvort_create_poisson(const ws_config_t* cfg, int32_t poisson, ws_bvort_t*
             ws::hck(hipMalloc(&b->ax, (size_t)nk * b->es()), "hipMalloc");
             ws::hck(hipMalloc(&b->ay, (size_t)b->H * b->es()), "hipMalloc");
             for (void* p : {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc})
-                ws::hck(hipMemsetAsync(p, 0, fb, b->stream), "hipMemsetAsync");  // ordered with the model's stream
+                ws::hck(hipMemsetAsync(p, 0, fb, b->stream), "hipMemsetAsync");
+            // the field uploads (ws_bvort_set_vorticity) use hipMemcpy, which is not ordered
+            // with the model's non-blocking stream: the zeroing must be complete first
+            ws::hck(hipStreamSynchronize(b->stream), "hipStreamSynchronize");
             const bool f64 = b->dtype == WS_F64;
             auto pow2 = [](int n) { return n >= 16 && n <= 4096 && (n & (n - 1)) == 0; };
             if (poisson != WS_POISSON_AUTO && poisson != WS_POISSON_HIPFFT) throw AbiError(WS_ERR_INVALID, "bad poisson mode");

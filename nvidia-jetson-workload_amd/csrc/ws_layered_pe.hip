@@ -241,6 +241,7 @@ namespace ws {
 namespace {
 
 void lpe_free(ws_lpe* m) {
+    if (m->stream) (void)hipStreamSynchronize(m->stream);  // nothing queued may touch freed memory
     for (int s = 0; s < 2; ++s)
         for (void* p : m->S[s])
             if (p) (void)hipFree(p);
@@ -367,8 +368,11 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
             for (int s = 0; s < 2; ++s)
                 for (void*& p : m->S[s]) {
                     ws::hck(hipMalloc(&p, fb), "hipMalloc");
-                    ws::hck(hipMemsetAsync(p, 0, fb, m->stream), "hipMemsetAsync");  // ordered with the model's stream
+                    ws::hck(hipMemsetAsync(p, 0, fb, m->stream), "hipMemsetAsync");
                 }
+            // the field uploads (ws_lpe_set_field) use hipMemcpy, which is not ordered with the
+            // model's non-blocking stream: the zeroing must be complete first
+            ws::hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
             for (void** grp : {m->A, m->B, m->acc})
                 for (int i = 0; i < 3; ++i) ws::hck(hipMalloc(&grp[i], fb), "hipMalloc");
             for (void*& p : m->tot) ws::hck(hipMalloc(&p, (size_t)m->H * m->W * m->es()), "hipMalloc");
