@@ -161,6 +161,12 @@ struct Cx {
 // LDS cycles where the round-2 "+1 per 16" padding had 6 912 + 9 920).
 __device__ __forceinline__ int P(int i) { return i ^ (((i >> 3) ^ (i >> 4) ^ (i >> 9)) & 31); }
 __host__ __device__ constexpr size_t padded(size_t n) { return (n + 31) / 32 * 32; }
+// Twiddle table slots: a pass reads tw[k * tstep] with k following the lanes, at strides of
+// 2 .. 128 entries -- with a plain table 8 to 16 lanes of a 32-lane group share a bank. Entry
+// k lives at k ^ ((k >> 5) & 31): for every stride 2^a (a = 1..7) the 32 lanes' slots are
+// distinct modulo 32 (their low index bits pass through, the bits shifted out of the low
+// five come back in by the xor). A permutation inside each aligned block of 32 entries.
+__device__ __forceinline__ int TW(int k) { return k ^ ((k >> 5) & 31); }
 
 __device__ __forceinline__ int bitrev(int i, int logn) { return (int)(__builtin_bitreverse32((uint32_t)i) >> (32 - logn)); }
 
@@ -194,7 +200,7 @@ __device__ __forceinline__ void dit_pass(Cx<T>* a, const Cx<T>* tw, int n, int l
 #pragma unroll
             for (int m = 0; m < M; ++m) {
                 if (m & hs) continue;
-                Cx<T> w = tw[(j + (m & (hs - 1)) * h) * tstep];
+                Cx<T> w = tw[TW((j + (m & (hs - 1)) * h) * tstep)];
                 if (INV) w.y = -w.y;
                 const Cx<T> v = x[m + hs];
                 const Cx<T> p{v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x};
@@ -230,7 +236,7 @@ __device__ __forceinline__ void dif_pass(Cx<T>* a, const Cx<T>* tw, int n, int l
 #pragma unroll
             for (int m = 0; m < M; ++m) {
                 if (m & hs) continue;
-                Cx<T> w = tw[(j + (m & (hs - 1)) * h) * tstep];
+                Cx<T> w = tw[TW((j + (m & (hs - 1)) * h) * tstep)];
                 if (INV) w.y = -w.y;
                 const Cx<T> u = x[m], v = x[m + hs];
                 const Cx<T> d{u.x - v.x, u.y - v.y};
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(kRowThreads) void bv_rowfft_fwd(const T* z, Cx<T>* 
     Cx<T>* twl = a + padded(W);  // twiddles staged in LDS: every pass reads them
     const int nk = W / 2;        // spectrum columns: k = 1 .. W/2-1, plus the packed real bins in column 0
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
-    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[i] = tw[i];
+    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[TW(i)] = tw[i];
     for (int i = threadIdx.x; i < W; i += kRowThreads) a[P(bitrev(i, logw))] = Cx<T>{z[r0 * W + i], z[r1 * W + i]};
     lds_barrier();
     fft_dit<T, false>(a, twl, W, logw, 1);
@@ -316,7 +322,7 @@ __global__ __launch_bounds__(kColThreads<T>) void bv_colsolve(Cx<T>* spec, const
     const int k0 = blk * cw;
     const int ncol = min(cw, nk - k0);
     const int t = threadIdx.x, nt = blockDim.x;
-    for (int i = t; i < H / 2; i += nt) twl[i] = tw[i];
+    for (int i = t; i < H / 2; i += nt) twl[TW(i)] = tw[i];
     for (int i = t; i < H * cw; i += nt) {
         const int l = i >> logcw, c = i & (cw - 1);
         if (c < ncol) a[P((c << logh) + bitrev(l, logh))] = spec[(int64_t)l * nk + k0 + c];
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(kRowThreads) void bv_rowfft_inv(const Cx<T>* spec, 
     Cx<T>* twl = a + padded(W);
     const int nk = W / 2;  // column 0 packs the real bins: A(0) + i A(W/2)
     const int64_t r0 = 2 * (int64_t)blockIdx.x, r1 = r0 + 1;
-    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[i] = tw[i];
+    for (int i = threadIdx.x; i < W / 2; i += kRowThreads) twl[TW(i)] = tw[i];
     // Z = A + i B over the Hermitian extension: bin k < W/2 gives Z(k) and Z(W - k); the real
     // bins (C2R: their imaginary parts are ignored) give Z(0) and Z(W/2). Each bin read once.
     for (int k = threadIdx.x; k < nk; k += kRowThreads) {
