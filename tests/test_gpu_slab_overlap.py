@@ -190,3 +190,23 @@ def test_create_slab_requires_an_id():
     st = _native.lib.ws_sim_create_slab(ctypes.byref(c._to_c()), 0, 2, None, ctypes.byref(h), ctypes.byref(r0),
                                         ctypes.byref(nr))
     assert st != 0 and "null communicator id" in _native.lib.ws_last_error().decode()
+
+
+@pytest.mark.parametrize("overlap", ["off", "on"])
+@pytest.mark.parametrize("nslabs", [3, 8])
+def test_fast_numerics_slabs_match_single_domain(nslabs, overlap, monkeypatch):
+    """The fp64 default (fast numerics) on slab groups, both schedules: bit-for-bit the
+    single-domain fast run (the decomposition changes no per-cell arithmetic), incl. the
+    autotuned kernel and launch width and a run ending mid-block."""
+    monkeypatch.setenv("WS_NUMERICS", "fast")
+    for k in ("WS_KERNEL", "WS_TB", "WS_SEG_ROWS", "WS_SLAB_OVERLAP"):
+        monkeypatch.delenv(k, raising=False)
+    c = lambda: _cfg(200, 8 * 48 + 5, 2, True)  # noqa: E731
+    one, group = _pair(c, nslabs, ws.JetStreamInitialCondition())
+    one.set_numerics("fast")
+    group.set_slab_schedule(0, overlap)
+    assert one.get_numerics() == "fast" and group.slab(0).get_numerics() == "fast"
+    for n in (13, 4):
+        assert group.run(n) == n
+        one.run(n)
+    _check(one, group)

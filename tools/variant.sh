@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build an A/B measurement variant of libws_hip.so with extra -D flags on one kernel file
-# (default ws_fused_dpp.hip = the DPP kernel's VGPR mode; ws_fused_dpp_dma.hip / _ldsy.hip
-# hold its other modes):
+# (default ws_fused_dppy_f64_2.hip = the fp64 two-step dppy / x2y instantiations; e.g.
+# ws_runtime.cpp with -DWS_PITCH_PAD=64 for a padded row pitch):
 #   tools/variant.sh NAME "-DWS_DPP_PF=5 ..." [file]  -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
 set -eu
 cd "$(dirname "$0")/../nvidia-jetson-workload_amd/csrc"
 make -s -j8 >/dev/null
-NAME=$1; DEFS=${2:-}; SRC=${3:-ws_fused_dpp.hip}
+NAME=$1; DEFS=${2:-}; SRC=${3:-ws_fused_dppy_f64_2.hip}
 mkdir -p _obj/var ../lib/variants
 FLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include -I/opt/rocm/include"
 /opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/$NAME.o
