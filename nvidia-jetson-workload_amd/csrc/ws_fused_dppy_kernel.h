@@ -153,7 +153,10 @@ struct StepRings {
 };
 
 template <typename T, int NST, int NSTEP, int MODE, int CPL>
-__global__ __launch_bounds__(kWave, 1) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+#ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
+#define WS_DPPY_MINW 1
+#endif
+__global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
     constexpr int kG = 16 / (int)sizeof(VT);               // rows per DMA instruction
