@@ -139,6 +139,14 @@ __device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& 
 #define WS_DPPY_LDSX -1
 #endif
 
+// Workgroup barrier ordering LDS traffic only (no global-memory fence: the DMA prefetch stays
+// in flight across it)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // s_waitcnt immediate for "vmcnt <= n" alone (gfx9 encoding: vmcnt[3:0], expcnt[6:4],
 // lgkmcnt[11:8], vmcnt[15:14]); the other counters at their maxima = not waited on
 constexpr int waitcnt_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
@@ -152,27 +160,45 @@ struct StepRings {
     V3<VT> O[2];                  // the step's last output rows (the next step's input), NSTEP > 1
 };
 
-template <typename T, int NST, int NSTEP, int MODE, int CPL>
+// SPLIT (two steps per launch, one column per lane; variant "pc"): a workgroup of two waves on
+// one strip and segment, wave 0 the producer of the first time step (LDS-DMA of y_n, its four
+// stages, its output rows into an LDS ring), wave 1 the consumer (the second step's stages from
+// that ring, the stores of y_{n+2}). Each wave holds one step's register rings, so the kernel
+// fits 4 waves per SIMD where the one-wave two-step march (221 VGPRs) fits 2. The consumer runs
+// kLag = 2 march bodies behind the producer; an LDS-only workgroup barrier every 2 bodies hands
+// the rows over (the consumer reads rows the producer finished before the last barrier, the
+// producer overwrites slots the consumer finished before it: kU >= 6 ring slots).
+constexpr int kLag = 2;
+
+template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
 #ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
 #define WS_DPPY_MINW 1
 #endif
-__global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs)
+#define WS_PC_MINW 4
+#endif
+__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? WS_PC_MINW : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
+    static_assert(!SPLIT || (NSTEP == 2 && CPL == 1), "producer / consumer: two steps, one column per lane");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
     constexpr int kG = 16 / (int)sizeof(VT);               // rows per DMA instruction
     // DMA rows in flight: WS_DPPY_PF groups ahead (0 = 4 rows; C2 two-step fp64: 0.1272 ->
     // 0.1162 ms/step at 4 rows against 2; C3 fp32 pairs: 0.0260 -> 0.0222 at 4 rows
-    // against 2, 0.0256 at 6)
-    constexpr int kPF = WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
+    // against 2, 0.0256 at 6). The producer's bodies are one step long: one group ahead.
+    constexpr int kPF = SPLIT ? 1 : WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
     constexpr int kD = kG * kPF;
     constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
     constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1
-    constexpr int kU = kNR;                                 // march unroll: ring slot == phase
+    // march unroll: ring slot == phase (SPLIT: >= 6, the handover ring's slots, see above)
+    constexpr int kU = SPLIT ? (6 + kNR - 1) / kNR * kNR : kNR;
     constexpr int kNS = NST * NSTEP;                        // stages per launch (the cone depth)
-    // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on
-    constexpr int kNW = (2 * kNS + kU - 1) / kU < 3 ? (2 * kNS + kU - 1) / kU : 3;
+    // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on (the
+    // consumer's bodies lag kLag rows). At most three are peeled: a stage computed before it
+    // enters the cone only reaches rows that are never stored (skipping it saves work only).
+    constexpr int kWarm = 2 * kNS + (SPLIT ? kLag : 0);
+    constexpr int kNW = (kWarm + kU - 1) / kU < 3 ? (kWarm + kU - 1) / kU : 3;
     // a group's DMA may overwrite only slots whose rows were read in an earlier body
-    static_assert(kU % kG == 0 && kU % 2 == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
+    static_assert(kU % kG == 0 && kU % 2 == 0 && kU % kNR == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
     static_assert(NSTEP == 1 || NSTEP == 2, "one or two steps per launch");
     // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory LOADS
     // issued after them (the DMAs in between, incl. the reading body's own). Stores are not
@@ -180,11 +206,14 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
     // drop below the threshold while the group is still in flight (seen as stale rows at
     // 4096^2). Loads complete in order.
     constexpr int kWaitN = 3 * (kD / kG);
-    constexpr unsigned kLdsX = (WS_DPPY_LDSX >= 0 ? (unsigned)(WS_DPPY_LDSX) : CPL == 1 ? 0x1u : 0x0u) & ((1u << kNS) - 1u);
+    constexpr unsigned kLdsX = ((WS_DPPY_LDSX >= 0 ? (unsigned)(WS_DPPY_LDSX) : CPL == 1 ? 0x1u : 0x0u) |
+                                (SPLIT ? 1u << NST : 0u)) & ((1u << kNS) - 1u);
     constexpr auto ldsx = [](int gs) { return ((kLdsX >> (gs - 1)) & 1u) != 0; };
     // LDS row slots of the stages (other than stage 1) that read neighbours from LDS
-    constexpr auto xslot = [](int gs) { return __builtin_popcount(kLdsX & ((1u << (gs - 1)) - 1u) & ~1u); };
-    constexpr int kNX = __builtin_popcount(kLdsX & ~1u);
+    // (SPLIT: the consumer's first stage reads the handover ring, no LDS row of its own)
+    constexpr unsigned kXRow = kLdsX & ~1u & ~(SPLIT ? 1u << NST : 0u);
+    constexpr auto xslot = [](int gs) { return __builtin_popcount(kXRow & ((1u << (gs - 1)) - 1u)); };
+    constexpr int kNX = __builtin_popcount(kXRow);
 
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
@@ -192,7 +221,9 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
     fused_rows(a, (w / nstrips) % nsegs, y0, y1);
     const int level = w / (nstrips * nsegs);
 
-    const int lane = (int)threadIdx.x;
+    const int lane = (int)threadIdx.x % kWave;
+    // SPLIT: wave 0 produces the first time step, wave 1 consumes it (wave-uniform)
+    const bool producer = !SPLIT || __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave) == 0;
     // left margin: the cone (kNS) rounded up to whole 16-byte chunks, so a strip's DMA chunks
     // never straddle column 0 (a partly negative chunk is dropped whole by the range check)
     constexpr int kC = 16 / (int)sizeof(T);  // columns per chunk
@@ -214,7 +245,8 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
     // (no exec-mask branch). launch_fused_step_dppy checks the byte ranges fit.
     const int64_t lofs = (int64_t)level * g.lstride;
     const int rbase = max(y0 - kNS, row_lo);
-    const int rtop = min(row_hi, y1 + kNS + kU + kD + kG);  // past the last row the march fetches
+    // past the last row the march fetches (SPLIT: kLag more bodies, see march)
+    const int rtop = min(row_hi, y1 + kNS + (SPLIT ? kLag : 0) + kU + kD + kG);
     const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
     const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
     const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
@@ -253,11 +285,14 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         lds_dma16(rh, &ring[2][slot][0], vo);
     };
     auto read_row = [&](int slot) -> V3<VT> { return V3<VT>{ring[0][slot][lane], ring[1][slot][lane], ring[2][slot][lane]}; };
+    // SPLIT: the handover ring of the first step's output rows, hring[field][slot][lane], slot =
+    // the producing body's march phase (row R - NST of the body at phase P goes to slot P)
+    __shared__ VT hring[3][SPLIT ? kU : 1][kWave];
     // per-wave LDS rows of the LDS-neighbour stages: xrow[parity][slot][field][lane]
     __shared__ VT xrow[2][kNX > 0 ? kNX : 1][3][kWave];
     auto xput = [&](auto Pc, auto GSc, const V3<VT>& v) {
         constexpr int P = decltype(Pc)::value, gs = decltype(GSc)::value;
-        if constexpr (gs > 1 && ldsx(gs)) {
+        if constexpr (gs > 1 && ldsx(gs) && !(SPLIT && gs == NST + 1)) {
             auto& b = xrow[P % 2][xslot(gs)];
             b[0][lane] = v.u;
             b[1][lane] = v.v;
@@ -270,8 +305,13 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         if constexpr (!ldsx(gs)) {
             dpp_lr3(mid, l, r);
         } else {
-            // stage 1: the mid row's ring slot; later stages: the previous body's LDS row
-            if constexpr (gs == 1) {
+            // stage 1: the mid row's ring slot; the consumer's first stage: the mid row's
+            // handover slot; later stages: the previous body's LDS row
+            if constexpr (SPLIT && gs == NST + 1) {
+                lds_lr(hring[0][rs], lane, mid.u, l.u, r.u);
+                lds_lr(hring[1][rs], lane, mid.v, l.v, r.v);
+                lds_lr(hring[2][rs], lane, mid.h, l.h, r.h);
+            } else if constexpr (gs == 1) {
                 lds_lr(ring[0][rs], lane, mid.u, l.u, r.u);
                 lds_lr(ring[1][rs], lane, mid.v, l.v, r.v);
                 lds_lr(ring[2][rs], lane, mid.h, l.h, r.h);
@@ -292,7 +332,8 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         for (int i = 0; i < 2; ++i) st[q].Y[i] = st[q].S1[i] = st[q].S2[i] = st[q].S3[i] = st[q].K2[i] = st[q].K3[i] = st[q].O[i] = Z;
 
     const int R0 = y0 - kNS;
-    const int R1 = R0 + (y1 + kNS - R0 + kU - 1) / kU * kU;  // rounded up to the unroll
+    // rounded up to the unroll (SPLIT: the consumer's bodies lag kLag rows behind the march)
+    const int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
 
     // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
     // stage s computes row Rq - s; the step's output row Rq - NST goes to `out`. Stage s of
@@ -313,7 +354,9 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         using S2c = std::integral_constant<int, 2>;
         using S3c = std::integral_constant<int, 3>;
         using S4c = std::integral_constant<int, 4>;
-        constexpr int rs1 = ((P - 1) % kNR + kNR) % kNR;  // ring slot of row R-1 (step 1's stage-1 mid)
+        // ring slot of row R-1 (step 1's stage-1 mid); the consumer's: the handover slot of the
+        // row produced one body before the one arriving (bodies lag kLag phases)
+        constexpr int rs1 = SPLIT && q == 1 ? ((P - kLag - 1) % kU + kU) % kU : ((P - 1) % kNR + kNR) % kNR;
         // stage 1's mid row next body (written even while stage 1 is outside the cone: the
         // next body may need it)
         xput(Pc, gsc(S1c{}), i0);
@@ -356,7 +399,7 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
                                 out = rk4_final<MODE>(S.Y[r2(-4)], a.c_dt6, k4, S.K2[r2(-4)], S.K3[r2(-4)]);
                             }
                             S.S3[r2(-3)] = s3;  // after k4 read S3[r2(-5)] (same slot)
-                            S.K3[r2(-3)] = rk4_keep3<MODE>(S.K2[r2(-3)], k3);
+                            S.K3[r2(-3)] = rk4_keep3<MODE>(S.Y[r2(-3)], a.c_dt6, S.K2[r2(-3)], k3);
                         }
                         S.S2[r2(-2)] = s2;  // after k3 read S2[r2(-4)] (same slot)
                         S.K2[r2(-2)] = k2;  // after the final combination read K2[r2(-4)]
@@ -404,19 +447,76 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         }
     };
 
-    auto march = [&](auto Xc, auto Yc) {
+    // SPLIT: the producer's body -- the first step at march row R, its output row R - NST into
+    // handover slot P (no store)
+    auto pbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr int KW = decltype(KWc)::value;
+        struct On {
+            constexpr bool operator()(int gs) const { return KW < 0 || KW * kU + P >= 2 * gs; }
+        };
+        constexpr auto sl = [](int d) { return ((P + d) % kNR + kNR) % kNR; };
+        if constexpr (P % kG == 0) {
+            dma(R + kD, sl(kD));
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));
+        }
+        const V3<VT> yR0 = read_row(sl(0)), yR1 = read_row(sl(-1)), yR2 = read_row(sl(-2));
+        __builtin_amdgcn_sched_barrier(0);
+        V3<VT> o0 = Z;
+        step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o0);
+        hring[0][P][lane] = o0.u;
+        hring[1][P][lane] = o0.v;
+        hring[2][P][lane] = o0.h;
+    };
+    // SPLIT: the consumer's body at the same phase -- march row R - kLag of the second step: its
+    // input rows from the handover slots the producer filled kLag .. kLag + 2 bodies ago, its
+    // output row stored
+    auto cbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr int KW = decltype(KWc)::value;
+        struct On {
+            constexpr bool operator()(int gs) const { return KW < 0 || KW * kU + P - kLag >= 2 * gs; }
+        };
+        constexpr auto hs = [](int d) { return ((P - kLag + d) % kU + kU) % kU; };
+        const V3<VT> i0{hring[0][hs(0)][lane], hring[1][hs(0)][lane], hring[2][hs(0)][lane]};
+        const V3<VT> i1{hring[0][hs(-1)][lane], hring[1][hs(-1)][lane], hring[2][hs(-1)][lane]};
+        const V3<VT> i2{hring[0][hs(-2)][lane], hring[1][hs(-2)][lane], hring[2][hs(-2)][lane]};
+        const int Rc = R - kLag;
+        V3<VT> o1 = Z;
+        step(std::integral_constant<int, 1>{}, Pc, Xc, Yc, On{}, st[1], i0, i1, i2, Rc - NST, o1);
+        if constexpr (On{}(2 * NST)) store_row(Rc - 2 * NST, o1);
+        else store_row(y0 - 1, Z);
+    };
+
+    // ROLE (SPLIT): the producer's or the consumer's march -- two loops, each carrying only its
+    // own step's register rings, passing the same barriers (the same periods)
+    auto march_role = [&](auto Xc, auto Yc, auto ROLEc) {
+        constexpr bool kProd = decltype(ROLEc)::value;
         // the kD virtual bodies before R0: DMAs for rows R0 .. R0 + kD - 1 and (dropped)
-        // stores, the same outstanding-op pattern the loop's back edge has
-        [&]<int... Vs>(std::integer_sequence<int, Vs...>) {
-            ([&] {
-                constexpr int v = Vs - kD;  // -kD .. -1
-                if constexpr (((v % kG) + kG) % kG == 0) dma(R0 + v + kD, v + kD);
-                store_row(y0 - 1, Z);
-            }(), ...);
-        }(std::make_integer_sequence<int, kD>{});
+        // stores, the same outstanding-op pattern the loop's back edge has (SPLIT: the
+        // producer's DMAs only)
+        if constexpr (kProd) {
+            [&]<int... Vs>(std::integer_sequence<int, Vs...>) {
+                ([&] {
+                    constexpr int v = Vs - kD;  // -kD .. -1
+                    if constexpr (((v % kG) + kG) % kG == 0) dma(R0 + v + kD, v + kD);
+                    if constexpr (!SPLIT) store_row(y0 - 1, Z);
+                }(), ...);
+            }(std::make_integer_sequence<int, kD>{});
+        }
         auto period = [&](auto KWc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-                (body(std::integral_constant<int, Ps>{}, Xc, Yc, KWc, R + Ps), ...);
+                ([&] {
+                    constexpr int P = Ps;
+                    if constexpr (!SPLIT) {
+                        body(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                    } else {
+                        // both waves pass every barrier: the branch is below it
+                        if constexpr (P % kLag == 0) lds_barrier();
+                        if constexpr (kProd) pbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                        else cbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                    }
+                }(), ...);
             }(std::make_integer_sequence<int, kU>{});
         };
         // warm-up periods (R1 - R0 >= kU: at least the first runs), then the steady march
@@ -427,6 +527,11 @@ __global__ __launch_bounds__(kWave, WS_DPPY_MINW) void fused_dppy_kernel(FusedAr
         }(std::make_integer_sequence<int, kNW>{});
         for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
+    };
+    auto march = [&](auto Xc, auto Yc) {
+        if constexpr (!SPLIT) march_role(Xc, Yc, std::true_type{});
+        else if (producer) march_role(Xc, Yc, std::true_type{});
+        else march_role(Xc, Yc, std::false_type{});
     };
     // global edges matter only to strips / segments within kNS cells of them
     const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - kNS;
@@ -452,11 +557,11 @@ constexpr unsigned kLdsPad = WS_DPPY_LDS_PAD;
 constexpr unsigned kLdsPad = 0;
 #endif
 
-template <typename T, int NSTEP, int CPL>
+template <typename T, int NSTEP, int CPL, bool SPLIT = false>
 hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
-    const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(kWave);
+    const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(SPLIT ? 2 * kWave : kWave);
 #define WS_DPPY_GO(N, M) \
-    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)
+    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)
 #define WS_DPPY_G1(M) WS_DPPY_GO(1, M)
 #define WS_DPPY_G2(M) WS_DPPY_GO(2, M)
 #define WS_DPPY_G4(M) WS_DPPY_GO(4, M)

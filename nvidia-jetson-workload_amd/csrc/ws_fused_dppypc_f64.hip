@@ -1,0 +1,11 @@
+// fused_dppy_kernel instantiations for double, two time steps per launch split over a producer and a
+// consumer wave (variant pc; see ws_fused_dppy_kernel.h, SPLIT)
+#include "ws_fused_dppy_kernel.h"
+
+namespace ws {
+template <typename T>
+hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
+    return launch_dppy_impl<T, 2, 1, true>(nstages, a, g, s, nstrips, nsegs);
+}
+template hipError_t launch_dppy_pc_tu<double>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
+}  // namespace ws
