@@ -27,7 +27,7 @@
  * Environment switches read by the library (all optional; everything else is an argument):
  *   WS_NUMERICS=exact|fast    numerics of the fused kernels at creation (ws_sim_set_numerics)
  *   WS_FUSED=0                per-stage kernels instead of the fused step kernel
- *   WS_KERNEL=x2y|dppy|pc|lds pin the fused-kernel variant      } each also settable per
+ *   WS_KERNEL=dppy|x2y|pc|pc2|lds (pin the fused-kernel variant)     } each also settable per
  *   WS_TB=1|2                 pin the steps per fused launch    } simulation with
  *   WS_SEG_ROWS=n             pin the rows per kernel segment   } ws_sim_pin_variant
  *   WS_AUTOTUNE=0|1|2         variant autotuner off / on (default) / on + print its table
@@ -344,7 +344,7 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
  * 5 = the same with an adjacent column pair per lane (128 columns per wave), 6 = the DPP
  * kernel's two-step launch split over a producer wave (the first step) and a consumer wave
  * (the second) per strip, handing rows over through LDS (its one-step launches are kernel
- * 4's), -1 = per-stage kernels (ids 1-3 are retired variants); seg_rows = output rows per segment, out_cols =
+ * 4's), 7 = the same split of kernel 5 (column pairs), -1 = per-stage kernels (ids 1-3 are retired variants); seg_rows = output rows per segment, out_cols =
  * output columns per strip (a multiple of the 128-byte line when the strips are
  * line-aligned). Chosen by timing every variant on the real grid at the first run (all give
  * identical results), unless WS_KERNEL / WS_SEG_ROWS / ws_sim_pin_variant fix it. The
@@ -354,12 +354,13 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
 int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols);
 
 /* Pin (part of) the fused-kernel variant of one simulation; -1 leaves a part to the
- * autotuner. kernel: WS_KERNEL_LDS / _DPPY / _X2Y / _PC; steps_per_launch: 1 or 2; seg_rows:
+ * autotuner. kernel: WS_KERNEL_LDS / _DPPY / _X2Y / _PC / _PC2; steps_per_launch: 1 or 2; seg_rows:
  * output rows per segment; align: 1 = strip output windows on whole 128-byte lines. */
 #define WS_KERNEL_LDS 0
 #define WS_KERNEL_DPPY 4
 #define WS_KERNEL_X2Y 5
 #define WS_KERNEL_PC 6
+#define WS_KERNEL_PC2 7
 int ws_sim_pin_variant(ws_sim_t* sim, int32_t kernel, int32_t steps_per_launch, int32_t seg_rows, int32_t align);
 
 /* Time steps per fused launch the simulation's run() uses where it can (new; temporal

@@ -28,10 +28,10 @@ static void autotune_time(ws_sim* s) {
     const int fixed_tb = s->tb;
     // two steps per launch only where a run can use them (slab blocks of >= 2 steps)
     const bool tb2_ok = s->block >= 2 || s->nranks == 1;
-    for (int k : {kKernDppLdsY, kKernX2Y, kKernPc, kKernLds})
+    for (int k : {kKernDppLdsY, kKernX2Y, kKernPc, kKernPc2, kKernLds})
       for (int tb : {1, 2}) {
         if (tb == 2 && (k == kKernLds || !tb2_ok)) continue;
-        if (tb == 1 && k == kKernPc) continue;  // a two-step split (its one-step launches are dppy's)
+        if (tb == 1 && ws::fused_split(k)) continue;  // a two-step split (its one-step launches are dppy's / x2y's)
         if (s->tb_fixed && k != kKernLds && tb != fixed_tb) continue;
         s->tb = tb;
         const int cone = nst * tb;
@@ -54,10 +54,10 @@ static void autotune_time(ws_sim* s) {
                 // extra wave
                 s->seg_override = 0;
                 std::vector<int> segs{s->seg_rows(nst)};
-                const int wave_per_block = k == kKernLds ? 4 : k == kKernPc ? 2 : 1;
+                const int wave_per_block = k == kKernLds ? 4 : ws::fused_split(k) ? 2 : 1;
                 for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
                     segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
-                if (k == kKernDppLdsY || k == kKernX2Y || k == kKernPc)  // more waves per SIMD fit: shorter segments pay
+                if (ws::fused_is_dppy(k))  // more waves per SIMD fit: shorter segments pay
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
@@ -199,8 +199,7 @@ static void tune_file_load_locked() {
     while (std::fscanf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d %d", &k.W, &k.H, &k.L, &k.dtype, &k.model,
                        &k.nst, &k.numerics, &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg, &c.align,
                        &c.tb) == 15)
-        if ((c.kernel == kKernLds || c.kernel == kKernDppLdsY || c.kernel == kKernX2Y || c.kernel == kKernPc) &&
-            (c.tb == 1 || c.tb == 2))
+        if ((c.kernel == kKernLds || ws::fused_is_dppy(c.kernel)) && (c.tb == 1 || c.tb == 2))
             g_tune_cache[k] = c;
     std::fclose(f);
 }

@@ -93,9 +93,10 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
 // one translation unit per (T, steps per launch, columns per lane): the kernel instantiations
 template <typename T, int NSTEP, int CPL>
 hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs);
-// "pc": the dppy kernel's two-step march split over a producer and a consumer wave
-// (ws_fused_dppy_kernel.h, SPLIT), one translation unit per T: ws_fused_dppypc_<t>.hip
-template <typename T>
+// "pc" / "pc2": the dppy / x2y kernel's two-step march split over a producer and a consumer
+// wave (ws_fused_dppy_kernel.h, SPLIT), one translation unit per (T, CPL):
+// ws_fused_dppypc{,2}_<t>.hip
+template <typename T, int CPL>
 hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone,
@@ -105,12 +106,18 @@ hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, 
 // is at most columns - 2 * margin, and when `aligned` it is rounded down to whole 128-byte
 // lines so no two strips write parts of one line. (Variant ids are ABI values,
 // ws_sim_fused_variant; 1-3 belonged to variants removed after never winning a config.)
-enum FusedVariant : int { kFusedLds = 0, kFusedDppLdsY = 4, kFusedX2Y = 5, kFusedPc = 6 };
+enum FusedVariant : int { kFusedLds = 0, kFusedDppLdsY = 4, kFusedX2Y = 5, kFusedPc = 6, kFusedPc2 = 7 };
+// the variants of the wave-independent kernel (ws_fused_dppy_kernel.h), and their lane width
+inline bool fused_is_dppy(int variant) {
+    return variant == kFusedDppLdsY || variant == kFusedX2Y || variant == kFusedPc || variant == kFusedPc2;
+}
+inline bool fused_pairs(int variant) { return variant == kFusedX2Y || variant == kFusedPc2; }
+inline bool fused_split(int variant) { return variant == kFusedPc || variant == kFusedPc2; }
 inline int fused_strip_cols(int variant) {
-    return variant == kFusedX2Y ? 128 : variant == kFusedDppLdsY || variant == kFusedPc ? 64 : 256;
+    return fused_pairs(variant) ? 128 : fused_is_dppy(variant) ? 64 : 256;
 }
 inline int fused_margin(int variant, int nstages, int elem_bytes) {
-    if (variant == kFusedDppLdsY || variant == kFusedX2Y || variant == kFusedPc) {
+    if (fused_is_dppy(variant)) {
         const int g = 16 / elem_bytes;
         return (nstages + g - 1) / g * g;
     }

@@ -8,14 +8,14 @@ template <typename T>
 hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g,
                                   hipStream_t s) {
     const int out_w = a.out_w;
-    if (variant != kFusedDppLdsY && variant != kFusedX2Y && variant != kFusedPc) return hipErrorInvalidValue;
+    if (!fused_is_dppy(variant)) return hipErrorInvalidValue;
     if (nsteps != 1 && nsteps != 2) return hipErrorInvalidValue;
     const int ns = nstages * nsteps;  // the launch's cone depth
     if (out_w < 1 || out_w > fused_strip_cols(variant) - 2 * fused_margin(variant, ns, (int)sizeof(T)))
         return hipErrorInvalidValue;
     if (out_w % (16 / (int)sizeof(T)) != 0) return hipErrorInvalidValue;  // chunk-aligned strips
     // column pairs are stored whole: an odd width's last pair ends in the row padding
-    if (variant == kFusedX2Y && (g.pitch % 2 != 0 || g.pitch < g.W + (g.W % 2))) return hipErrorInvalidValue;
+    if (fused_pairs(variant) && (g.pitch % 2 != 0 || g.pitch < g.W + (g.W % 2))) return hipErrorInvalidValue;
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (nsegs <= 0) return hipSuccess;
@@ -25,10 +25,12 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     // dropped-store voffset is 2^31
     const int64_t span = (int64_t)(a.seg_rows + 2 * ns + 48) * g.pitch * (int64_t)sizeof(T);
     if (span >= 0x7fffffff) return hipErrorInvalidValue;
-    // pc splits a two-step launch; its one-step launches (a run's odd step, a slab block's
-    // last) are the dppy kernel's, on the same strips
-    if (variant == kFusedPc && nsteps == 2) return launch_dppy_pc_tu<T>(nstages, a, g, s, nstrips, nsegs);
-    if (variant == kFusedX2Y)
+    // pc / pc2 split a two-step launch; their one-step launches (a run's odd step, a slab
+    // block's last) are the dppy / x2y kernel's, on the same strips
+    if (fused_split(variant) && nsteps == 2)
+        return fused_pairs(variant) ? launch_dppy_pc_tu<T, 2>(nstages, a, g, s, nstrips, nsegs)
+                                    : launch_dppy_pc_tu<T, 1>(nstages, a, g, s, nstrips, nsegs);
+    if (fused_pairs(variant))
         return nsteps == 1 ? launch_dppy_tu<T, 1, 2>(nstages, a, g, s, nstrips, nsegs)
                            : launch_dppy_tu<T, 2, 2>(nstages, a, g, s, nstrips, nsegs);
     return nsteps == 1 ? launch_dppy_tu<T, 1, 1>(nstages, a, g, s, nstrips, nsegs)

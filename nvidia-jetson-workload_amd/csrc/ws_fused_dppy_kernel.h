@@ -170,22 +170,28 @@ struct StepRings {
 // producer overwrites slots the consumer finished before it: kU >= 6 ring slots).
 constexpr int kLag = 2;
 
+#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), pairs 2
+#define WS_PC_MINW 0
+#endif
+constexpr int pc_min_waves(int cpl) { return WS_PC_MINW > 0 ? WS_PC_MINW : cpl == 1 ? 4 : 2; }
 template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
 #ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
 #define WS_DPPY_MINW 1
 #endif
-#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs)
-#define WS_PC_MINW 4
+#ifndef WS_PC_PF  // the producer's LDS-DMA prefetch distance in groups (0: 2 rows)
+#define WS_PC_PF 0
 #endif
-__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? WS_PC_MINW : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL) : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
-    static_assert(!SPLIT || (NSTEP == 2 && CPL == 1), "producer / consumer: two steps, one column per lane");
+    static_assert(!SPLIT || NSTEP == 2, "producer / consumer: a two-step launch");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
     constexpr int kG = 16 / (int)sizeof(VT);               // rows per DMA instruction
     // DMA rows in flight: WS_DPPY_PF groups ahead (0 = 4 rows; C2 two-step fp64: 0.1272 ->
     // 0.1162 ms/step at 4 rows against 2; C3 fp32 pairs: 0.0260 -> 0.0222 at 4 rows
-    // against 2, 0.0256 at 6). The producer's bodies are one step long: one group ahead.
-    constexpr int kPF = SPLIT ? 1 : WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
+    // against 2, 0.0256 at 6). The producer's bodies are one step long: at least 2 rows ahead
+    // (fp64 / fp32 pairs: one group; fp64 pairs: two).
+    constexpr int kPF = SPLIT ? (WS_PC_PF > 0 ? WS_PC_PF : (2 / kG > 1 ? 2 / kG : 1))
+                              : WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
     constexpr int kD = kG * kPF;
     constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
     constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1

@@ -1,5 +1,5 @@
 // fused_dppy_kernel instantiations for double, two time steps per launch split over a producer and a
-// consumer wave, one column per lane (variant pc; see ws_fused_dppy_kernel.h, SPLIT)
+// consumer wave, a column pair per lane (variant pc2; see ws_fused_dppy_kernel.h, SPLIT)
 #include "ws_fused_dppy_kernel.h"
 
 namespace ws {
@@ -7,5 +7,5 @@ template <typename T, int CPL>
 hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
     return launch_dppy_impl<T, 2, CPL, true>(nstages, a, g, s, nstrips, nsegs);
 }
-template hipError_t launch_dppy_pc_tu<double, 1>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
+template hipError_t launch_dppy_pc_tu<double, 2>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
 }  // namespace ws

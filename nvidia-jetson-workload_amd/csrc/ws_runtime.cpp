@@ -116,7 +116,7 @@ int32_t ws_sim::seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) c
 
 int32_t ws_sim::seg_rows(int nst) const {
     if (seg_override > 0) return seg_override;
-    const int64_t want_blocks = kernel == wsr::kKernX2Y ? 2048 : kernel == wsr::kKernDppLdsY || kernel == wsr::kKernPc ? 4096 : 512;
+    const int64_t want_blocks = ws::fused_pairs(kernel) ? 2048 : ws::fused_is_dppy(kernel) ? 4096 : 512;
     return seg_for_blocks(nst, want_blocks, 24 * nst);
 }
 
@@ -174,13 +174,13 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             s->numerics = std::strcmp(e, "fast") == 0 ? WS_NUMERICS_FAST : WS_NUMERICS_EXACT;
         }
         if (const char* e = env_str("WS_KERNEL")) {
-            require(std::strcmp(e, "lds") == 0 || std::strcmp(e, "dppy") == 0 || std::strcmp(e, "x2y") == 0 ||
-                        std::strcmp(e, "pc") == 0,
-                    WS_ERR_INVALID, "WS_KERNEL must be x2y, dppy, pc or lds");
-            s->kernel = std::strcmp(e, "lds") == 0    ? kKernLds
-                        : std::strcmp(e, "dppy") == 0 ? kKernDppLdsY
-                        : std::strcmp(e, "pc") == 0   ? kKernPc
-                                                      : kKernX2Y;
+            static const std::pair<const char*, int> names[] = {
+                {"lds", kKernLds}, {"dppy", kKernDppLdsY}, {"x2y", kKernX2Y}, {"pc", kKernPc}, {"pc2", kKernPc2}};
+            int k = -1;
+            for (const auto& n : names)
+                if (std::strcmp(e, n.first) == 0) k = n.second;
+            require(k >= 0, WS_ERR_INVALID, "WS_KERNEL must be x2y, dppy, pc, pc2 or lds");
+            s->kernel = k;
             s->kernel_fixed = true;
         }
         if (const char* e = env_str("WS_TB")) {
@@ -863,8 +863,8 @@ int ws_sim_get_numerics(const ws_sim_t* s, int32_t* mode) {
 int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, int32_t seg_rows, int32_t align) {
     return guarded([&] {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
-        require(kernel == -1 || kernel == kKernLds || kernel == kKernDppLdsY || kernel == kKernX2Y || kernel == kKernPc,
-                WS_ERR_INVALID, "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y or WS_KERNEL_PC");
+        require(kernel == -1 || kernel == kKernLds || ws::fused_is_dppy(kernel), WS_ERR_INVALID,
+                "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y, WS_KERNEL_PC or WS_KERNEL_PC2");
         require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2, WS_ERR_INVALID,
                 "steps_per_launch must be -1, 1 or 2");
         require(seg_rows == -1 || seg_rows > 0, WS_ERR_INVALID, "seg_rows must be -1 or positive");

@@ -102,7 +102,7 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
     const ws::Geom g = c->geom();
-    if (nsteps > 1 && s->kernel == kKernLds) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy, x2y or pc");
+    if (nsteps > 1 && s->kernel == kKernLds) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy, x2y, pc or pc2");
     if (s->kernel == kKernLds) WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st));
     else WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(s->kernel, nst, nsteps, a, g, st));
     ++s->last_launches;

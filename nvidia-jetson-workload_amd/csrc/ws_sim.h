@@ -145,7 +145,8 @@ ws::Spacing<T> make_spacing(double dx, double dy) {
     return s;
 }
 
-enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDppLdsY = ws::kFusedDppLdsY, kKernX2Y = ws::kFusedX2Y, kKernPc = ws::kFusedPc };
+enum FusedKernel : int { kKernLds = ws::kFusedLds, kKernDppLdsY = ws::kFusedDppLdsY, kKernX2Y = ws::kFusedX2Y, kKernPc = ws::kFusedPc,
+                         kKernPc2 = ws::kFusedPc2 };
 
 // slab schedule choice (ws_sim::overlap_mode)
 enum OverlapMode : int { kOverlapOff = 0, kOverlapOn = 1, kOverlapAuto = 2 };

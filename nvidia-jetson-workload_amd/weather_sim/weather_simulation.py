@@ -682,7 +682,7 @@ class WeatherSimulation:
         in use (chosen at the first run)."""
         k, seg, cols = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg), ctypes.byref(cols)))
-        return ({-1: "stage_kernels", 0: "fused_lds", 4: "fused_dppy", 5: "fused_x2y", 6: "fused_pc"}[k.value], seg.value,
+        return ({-1: "stage_kernels", 0: "fused_lds", 4: "fused_dppy", 5: "fused_x2y", 6: "fused_pc", 7: "fused_pc2"}[k.value], seg.value,
                 cols.value)
 
     def get_cfl(self, per_level=False, with_time=False):
@@ -713,7 +713,7 @@ class WeatherSimulation:
         return b.value, bool(o.value)
 
     _OVERLAP = {"off": 0, "on": 1, "auto": 2, False: 0, True: 1}
-    _KERNELS = {"lds": 0, "dppy": 4, "x2y": 5, "pc": 6}
+    _KERNELS = {"lds": 0, "dppy": 4, "x2y": 5, "pc": 6, "pc2": 7}
 
     def set_slab_schedule(self, block=0, overlap="auto"):
         """Extension: steps per halo exchange (block > 0; 0 keeps it) and the overlap schedule

@@ -73,7 +73,7 @@ def _fields(grid):
 
 
 @pytest.mark.parametrize("ic,kernel,tb", [("jet_stream", None, None), ("random", "dppy", "1"), ("random", "dppy", "2"),
-                                          ("random", "x2y", "2"), ("random", "pc", "2")])
+                                          ("random", "x2y", "2"), ("random", "pc", "2"), ("random", "pc2", "2")])
 def test_c5_single_gpu_matches_reference_bands(ic, kernel, tb, monkeypatch):
     if tb:
         monkeypatch.setenv("WS_KERNEL", kernel)

@@ -62,9 +62,9 @@ def test_default_numerics_by_precision(monkeypatch):
         s.set_numerics("approximate")
 
 
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"),
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"),
                                       ("lds", "1")],
-                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "lds"])
+                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"])
 def test_fast_matches_reference_fixtures(kernel, tb, monkeypatch):
     monkeypatch.setenv("WS_NUMERICS", "fast")
     monkeypatch.setenv("WS_KERNEL", kernel)

@@ -58,12 +58,12 @@ def load(sim, s0):
 
 # (WS_FUSED, WS_KERNEL, WS_TB): every fused variant, dppy also with two steps per launch
 # (temporal blocking: run(n) advances pairs of steps per launch), and the per-stage kernels
-KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "x2y", "2"), ("1", "pc", "2"),
+KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "x2y", "2"), ("1", "pc", "2"), ("1", "pc2", "2"),
            ("1", "lds", "1"), ("0", "x2y", "1")]
-KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_x2y_tb2", "fused_pc_tb2", "fused_lds", "stage_kernels"]
+KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_x2y_tb2", "fused_pc_tb2", "fused_pc2_tb2", "fused_lds", "stage_kernels"]
 # (kernel, steps per launch) of the fused variants
-FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("lds", "1")]
-FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "lds"]
+FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"), ("lds", "1")]
+FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"]
 
 
 @pytest.mark.parametrize("fused,kernel,tb", KERNELS, ids=KERNEL_IDS)
@@ -234,15 +234,15 @@ def _dam_break(W, H, width_cells, dtype):
     return np.broadcast_to(row, (H, W)).astype(dtype)
 
 
-@pytest.mark.parametrize("tb", ["1", "2", "pc"])
+@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2"])
 @pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
                                   "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
                                   "C3_zonal_flow_2048_baro_f32"])
 def test_full_size_digests(name, tb, monkeypatch):
-    """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, pc
-    the producer / consumer split of them."""
-    if tb in ("2", "pc"):
-        monkeypatch.setenv("WS_KERNEL", "dppy" if tb == "2" else "pc")
+    """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, pc /
+    pc2 the producer / consumer split of them (one column / a column pair per lane)."""
+    if tb in ("2", "pc", "pc2"):
+        monkeypatch.setenv("WS_KERNEL", "dppy" if tb == "2" else tb)
         monkeypatch.setenv("WS_TB", "2")
     d = large_digests()[name]
     spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
@@ -382,7 +382,7 @@ def test_fused_non_pow2_spacing_vs_oracle():
 
 @pytest.mark.parametrize("kernel,seg_rows,tb", [("dppy", "6", "1"), ("dppy", "0", "1"), ("dppy", "6", "2"),
                                                  ("dppy", "0", "2"), ("x2y", "6", "1"), ("x2y", "0", "1"),
-                                                 ("x2y", "6", "2"), ("pc", "6", "2"), ("pc", "0", "2"),
+                                                 ("x2y", "6", "2"), ("pc", "6", "2"), ("pc", "0", "2"), ("pc2", "6", "2"),
                                                  ("lds", "6", "1"), ("lds", "0", "1")])
 @pytest.mark.parametrize("nslabs", [2, 3, 5])
 @pytest.mark.parametrize("method", [0, 1, 2])

@@ -50,7 +50,7 @@ def _check(one, group, names=("u", "v", "h", "vorticity", "divergence")):
     assert group.slab(group.nslabs - 1).get_current_time() == one.get_current_time()
 
 
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "2"), ("pc", "2"), ("lds", "1")])
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"), ("lds", "1")])
 @pytest.mark.parametrize("block", ["1", "2", "3", "6"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 def test_overlap_group_matches_single_domain(method, block, kernel, tb, monkeypatch):

@@ -50,9 +50,9 @@ def test_strip_widths(W, kernel, tb, method, fp64, monkeypatch):
     run_both(W, 29, method, fp64, 5)
 
 
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"),
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"),
                                       ("lds", "1")],
-                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "lds"])
+                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 def test_non_pow2_spacing(kernel, tb, method, monkeypatch):
     monkeypatch.setenv("WS_KERNEL", kernel)
@@ -61,9 +61,9 @@ def test_non_pow2_spacing(kernel, tb, method, monkeypatch):
 
 
 @pytest.mark.parametrize("W", [61, 300, 700])
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"),
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"),
                                       ("lds", "1")],
-                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "lds"])
+                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_line_aligned_strips(W, kernel, tb, method, fp64, monkeypatch):

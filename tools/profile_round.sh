@@ -12,15 +12,15 @@ timeout -k 10 400 python bench.py --config $CFG --method $METHOD --steps $STEPS 
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; }
 read KERN KNAME SEG ALIGN TB < <(python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))['roofline']
-k={'fused_dppy':'dppy','fused_x2y':'x2y','fused_pc':'pc','fused_lds':'lds'}.get(d['kernel'],'dppy')
-n={'dppy':'fused_dppy_kernel','x2y':'fused_dppy_kernel','pc':'fused_dppy_kernel','lds':'fused_step_kernel'}[k]
+k={'fused_dppy':'dppy','fused_x2y':'x2y','fused_pc':'pc','fused_pc2':'pc2','fused_lds':'lds'}.get(d['kernel'],'dppy')
+n={'dppy':'fused_dppy_kernel','x2y':'fused_dppy_kernel','pc':'fused_dppy_kernel','pc2':'fused_dppy_kernel','lds':'fused_step_kernel'}[k]
 tb=d.get('steps_per_launch') or 1
 nst={'euler':1,'rk2':2,'rk4':4}['$METHOD']
 nst=2 if nst==4 and '$CFG' in ('c3','c4') else nst
 cone=nst*tb
 g=16//(8 if '$CFG' in ('c2','c5') or '$CFG'.startswith('c2_') else 4)
-margin=(cone+g-1)//g*g if k in ('dppy','x2y','pc') else cone
-full={'dppy':64,'x2y':128,'pc':64,'lds':256}[k]-2*margin
+margin=(cone+g-1)//g*g if k in ('dppy','x2y','pc','pc2') else cone
+full={'dppy':64,'x2y':128,'pc':64,'pc2':128,'lds':256}[k]-2*margin
 print(k, n, d.get('seg_rows') or 0, 1 if (d.get('strip_out_cols') or full) != full else 0, tb)")
 PIN="$KERN:$TB:$SEG:$ALIGN"
 echo "pinned: --pin $PIN (kernel:steps per launch:seg rows:align)"
