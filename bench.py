@@ -556,13 +556,16 @@ def main():
     achieved = bpl / (tot_ms / n * 1e-3) / 1e9
     step_bytes = sum(b for (_, _, b) in stats.values()) / tb  # one launch per kind covers tb steps
     # PMC of the same variant (tools/profile_round.sh -> profiles/traffic_<config>_<method>.json):
-    # HBM bytes and VALU wave-instructions per launch
-    traffic, valu_insts = None, None
+    # HBM bytes and VALU wave-instructions per launch -- used only when the profiled variant
+    # (kernel, steps per launch) is the one this run's autotuner chose
+    traffic, valu_insts, traffic_variant = None, None, None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
     if os.path.exists(tfile) and world == 1:
         with open(tfile) as f:
             tj = json.load(f)
-        traffic, valu_insts = tj.get(f"kind{kind}"), tj.get("valu_insts")
+        traffic_variant = tj.get("variant")
+        if traffic_variant is None or traffic_variant == {"kernel": variant.replace("fused_", ""), "tb": tb}:
+            traffic, valu_insts = tj.get(f"kind{kind}"), tj.get("valu_insts")
     launch_s = tot_ms / n * 1e-3
     # compulsory bytes of one launch: y_n read + y_(n+k) written once (6 words per cell, the
     # k steps in between never leave the chip)
@@ -601,6 +604,7 @@ def main():
                                   "launch it can exceed 1 -- the measured utilisations are compulsory_frac, "
                                   "dram_frac and valu_frac",
                      "traffic": traffic,
+                     "traffic_variant": traffic_variant,
                      "compulsory_gbs": compulsory / launch_s / 1e9,
                      "compulsory_frac": compulsory / launch_s / 1e9 / HBM_PEAK_GBS,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",

@@ -38,3 +38,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
 done
 python3 "$R/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc_summary.txt"
 python3 "$R/tools/traffic.py" "$OUT/pmc" "$KNAME" "$OUT/traffic_${CFG}_${METHOD}.json"
+# the profiled variant: bench.py uses these counters only for runs of the same kernel and steps per launch
+python3 -c "
+import json; p='$OUT/traffic_${CFG}_${METHOD}.json'; d=json.load(open(p))
+d['variant'] = {'kernel': '$KERN', 'tb': $TB}; d['pin'] = '$PIN'; json.dump(d, open(p, 'w'))"

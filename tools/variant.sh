@@ -6,11 +6,16 @@
 set -eu
 cd "$(dirname "$0")/../nvidia-jetson-workload_amd/csrc"
 make -s -j8 >/dev/null
-NAME=$1; DEFS=${2:-}; SRC=${3:-ws_fused_dppy_f64_2.hip}
+NAME=$1; DEFS=${2:-}; SRCS=${3:-ws_fused_dppy_f64_2.hip}  # one or more sources, space separated
 mkdir -p _obj/var ../lib/variants
 FLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include -I/opt/rocm/include"
-/opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/$NAME.o
-OBJS=$(ls _obj/*.o | grep -v "/${SRC}.o$")
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/variants/libws_hip_$NAME.so $OBJS _obj/var/$NAME.o \
+OBJS=$(ls _obj/*.o)
+VOBJS=""
+for SRC in $SRCS; do
+  /opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/${NAME}_$SRC.o
+  OBJS=$(echo "$OBJS" | grep -v "/${SRC}.o$")
+  VOBJS="$VOBJS _obj/var/${NAME}_$SRC.o"
+done
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../lib/variants/libws_hip_$NAME.so $OBJS $VOBJS \
     -L/opt/rocm/lib -lrccl -lhipfft -Wl,-rpath,/opt/rocm/lib
 echo "built lib/variants/libws_hip_$NAME.so"
