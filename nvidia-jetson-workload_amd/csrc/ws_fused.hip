@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
                             }
                             pub(Q3c{}, s3);
                             S3[r2(-3)] = s3;
-                            K3[r2(-3)] = rk4_keep3<MODE>(Y[yi(-3)], a.c_dt6, K2[r2(-3)], k3);
+                            K3[r2(-3)] = rk4_keep3<MODE>(K2[r2(-3)], k3);
                         } else {
                             store_row(y0 - 1, Z);
                         }

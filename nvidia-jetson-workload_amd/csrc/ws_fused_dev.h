@@ -144,39 +144,24 @@ __device__ __forceinline__ V3<VT> axpy(const V3<VT>& y, T c, const V3<VT>& k) {
 }
 
 // RK4-as-implemented: what the stage-3 ring keeps for the final combination -- k3 (exact), or
-// (fast numerics) the accumulator y + c (k2 + k3) formed at stage 3's row, so that the final
-// combination one row later needs neither y nor k2 (their rings shrink to the one row stage 3
-// reads: 12 fewer VGPRs per time step of a launch). With WS_RK4_ACC=0 (measurement builds) the
-// fast form keeps the running sum k2 + k3 instead and the final combination adds y.
-#ifndef WS_RK4_ACC
-#define WS_RK4_ACC 1
-#endif
-template <int MODE, typename VT, typename T>
-__device__ __forceinline__ V3<VT> rk4_keep3(const V3<VT>& y, T c, const V3<VT>& k2, const V3<VT>& k3) {
-    if constexpr (MODE >= kSpFast) {
-        if constexpr (WS_RK4_ACC) {
-            const VT cv = (VT)c;
-            return {fmadd(cv, k2.u + k3.u, y.u), fmadd(cv, k2.v + k3.v, y.v), fmadd(cv, k2.h + k3.h, y.h)};
-        } else {
-            return {k2.u + k3.u, k2.v + k3.v, k2.h + k3.h};
-        }
-    } else {
-        return k3;
-    }
+// the running sum k2 + k3 (fast numerics). (Round 3 measured an accumulator y + dt/3 (k2 + k3)
+// kept instead, which frees the y ring one row earlier: 1.5-2 % faster, but v of the C2 case
+// drifted to 3.2e-11 relative L2 from the exact run after 13 steps against 1.3e-16 -- not kept.)
+template <int MODE, typename VT>
+__device__ __forceinline__ V3<VT> rk4_keep3(const V3<VT>& k2, const V3<VT>& k3) {
+    if constexpr (MODE >= kSpFast) return {k2.u + k3.u, k2.v + k3.v, k2.h + k3.h};
+    else return k3;
 }
 
 // The final combination (k1 aliases k4, weather_simulation.cpp:437-451):
-// exact: y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4); fast: kept + dt/3 * k4, kept = y + dt/3 (k2 + k3)
-// (c = a.c_dt6, which prepare_fast turns into dt/3 * s). y and k2 are read in exact numerics only.
+// exact: y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4); fast: y + dt/3 * (kept + k4), kept = k2 + k3
+// (c = a.c_dt6, which prepare_fast turns into dt/3 * s)
 template <int MODE, typename VT, typename T>
 __device__ __forceinline__ V3<VT> rk4_final(const V3<VT>& y, T c, const V3<VT>& k4, const V3<VT>& k2,
                                             const V3<VT>& kept3) {
     if constexpr (MODE >= kSpFast) {
         const VT cv = (VT)c;
-        if constexpr (WS_RK4_ACC)
-            return {fmadd(cv, k4.u, kept3.u), fmadd(cv, k4.v, kept3.v), fmadd(cv, k4.h, kept3.h)};
-        else
-            return {fmadd(cv, kept3.u + k4.u, y.u), fmadd(cv, kept3.v + k4.v, y.v), fmadd(cv, kept3.h + k4.h, y.h)};
+        return {fmadd(cv, kept3.u + k4.u, y.u), fmadd(cv, kept3.v + k4.v, y.v), fmadd(cv, kept3.h + k4.h, y.h)};
     } else {
         const T two = T(2);
         V3<VT> o;

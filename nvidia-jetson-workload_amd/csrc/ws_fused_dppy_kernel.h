@@ -405,7 +405,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                                 out = rk4_final<MODE>(S.Y[r2(-4)], a.c_dt6, k4, S.K2[r2(-4)], S.K3[r2(-4)]);
                             }
                             S.S3[r2(-3)] = s3;  // after k4 read S3[r2(-5)] (same slot)
-                            S.K3[r2(-3)] = rk4_keep3<MODE>(S.Y[r2(-3)], a.c_dt6, S.K2[r2(-3)], k3);
+                            S.K3[r2(-3)] = rk4_keep3<MODE>(S.K2[r2(-3)], k3);
                         }
                         S.S2[r2(-2)] = s2;  // after k3 read S2[r2(-4)] (same slot)
                         S.K2[r2(-2)] = k2;  // after the final combination read K2[r2(-4)]
