@@ -130,10 +130,18 @@ static void autotune_time(ws_sim* s) {
     std::vector<Cand*> top;
     for (Cand& c : cands) top.push_back(&c);
     std::sort(top.begin(), top.end(), [](const Cand* a, const Cand* b) { return a->ms < b->ms; });
-    // the new neighbours (ms = 0) sort first; keep them and the three fastest timed ones
+    // the new neighbours (ms = 0) sort first; keep them, the three fastest timed ones, and the
+    // fastest of every other kernel variant (variants within a few % of each other -- dppy /
+    // pc at C2 -- were decided by one short window's noise)
     size_t keep = 0;
     while (keep < top.size() && top[keep]->ms == 0.f) ++keep;
-    if (top.size() > keep + 3) top.resize(keep + 3);
+    if (top.size() > keep + 3) {
+        std::vector<Cand*> rest(top.begin() + keep + 3, top.end());
+        top.resize(keep + 3);
+        for (Cand* c : rest)
+            if (std::none_of(top.begin(), top.end(), [&](const Cand* t) { return t->kernel == c->kernel; }))
+                top.push_back(c);
+    }
     if (top.size() > 1) {
         std::vector<float> sum(top.size(), 0.f);
         const int long_reps = std::max(reps, 16);
