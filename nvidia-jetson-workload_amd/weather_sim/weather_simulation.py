@@ -682,8 +682,8 @@ class WeatherSimulation:
         in use (chosen at the first run)."""
         k, seg, cols = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib.ws_sim_fused_variant(self._h, ctypes.byref(k), ctypes.byref(seg), ctypes.byref(cols)))
-        return ({-1: "stage_kernels", 0: "fused_lds", 4: "fused_dppy", 5: "fused_x2y", 6: "fused_pc", 7: "fused_pc2"}[k.value], seg.value,
-                cols.value)
+        names = {v: "fused_" + n for n, v in self._KERNELS.items()}
+        return names.get(k.value, "stage_kernels"), seg.value, cols.value
 
     def get_cfl(self, per_level=False, with_time=False):
         """Extension: the CFL number max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy)
