@@ -269,14 +269,14 @@ def test_full_size_digests(name, tb, monkeypatch):
                         f"|ref|={ref_l2!r})")
 
 
-@pytest.mark.parametrize("tb", ["0", "2"])
-def test_pe_levels_match_reference_per_level(tb, monkeypatch):
+@pytest.mark.parametrize("kernel,tb", [(None, "0"), ("dppy", "2"), ("x2y", "2"), ("pc", "2"), ("pc2", "2")])
+def test_pe_levels_match_reference_per_level(kernel, tb, monkeypatch):
     """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
     must equal a standalone reference run of that level (bitwise) -- the T / P update on
-    the second stream, with the autotuned kernel and with two steps per launch (dppy, two
-    T / P updates per launch)."""
-    if tb != "0":
-        monkeypatch.setenv("WS_KERNEL", "dppy")
+    the second stream, with the autotuned kernel and with two steps per launch (every
+    two-step variant, two T / P updates per launch)."""
+    if kernel:
+        monkeypatch.setenv("WS_KERNEL", kernel)
         monkeypatch.setenv("WS_TB", tb)
     digests = large_digests()
     L = 32
