@@ -170,10 +170,10 @@ struct StepRings {
 // producer overwrites slots the consumer finished before it: kU >= 6 ring slots).
 constexpr int kLag = 2;
 
-#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), pairs 2
+#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), fp64 pairs 2
 #define WS_PC_MINW 0
 #endif
-constexpr int pc_min_waves(int cpl) { return WS_PC_MINW > 0 ? WS_PC_MINW : cpl == 1 ? 4 : 2; }
+constexpr int pc_min_waves(int cpl, int elem) { return WS_PC_MINW > 0 ? WS_PC_MINW : cpl == 2 && elem == 8 ? 2 : 4; }
 template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
 #ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
 #define WS_DPPY_MINW 1
@@ -181,7 +181,7 @@ template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
 #ifndef WS_PC_PF  // the producer's LDS-DMA prefetch distance in groups (0: 2 rows)
 #define WS_PC_PF 0
 #endif
-__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL) : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL, (int)sizeof(T)) : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
     static_assert(!SPLIT || NSTEP == 2, "producer / consumer: a two-step launch");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
