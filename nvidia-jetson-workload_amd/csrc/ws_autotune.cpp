@@ -114,10 +114,18 @@ static void autotune_time(ws_sim* s) {
     // segment length a few % slower in a run (C2: seg 48 over 88, -4 %)
     // plus the segment lengths next to the best one (+-8, +-16 rows: the march constraint
     // seg + 2 cone = 0 mod 8 keeps them valid) when the heuristic list skipped them
-    {
-        const Cand b = *std::min_element(cands.begin(), cands.end(),
-                                         [](const Cand& x, const Cand& y) { return x.ms < y.ms; });
-        if (!s->seg_fixed)
+    // (around the best candidate of the two fastest kernel variants: dppy and pc at C2 are within
+    // a few % of each other, each at its own segment length)
+    if (!s->seg_fixed) {
+        std::vector<Cand> best2;
+        for (const Cand& c : cands) {
+            auto it = std::find_if(best2.begin(), best2.end(), [&](const Cand& b) { return b.kernel == c.kernel; });
+            if (it == best2.end()) best2.push_back(c);
+            else if (c.ms < it->ms) *it = c;
+        }
+        std::sort(best2.begin(), best2.end(), [](const Cand& x, const Cand& y) { return x.ms < y.ms; });
+        if (best2.size() > 2) best2.resize(2);
+        for (const Cand& b : best2)
             for (int d : {-16, -8, 8, 16}) {
                 const int seg = b.seg + d;
                 if (seg < 8 || seg > s->slot[0]->H) continue;
