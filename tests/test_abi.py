@@ -167,3 +167,14 @@ def test_environment_switches_are_few_and_documented():
     assert 0 < len(names) <= 8, sorted(names)
     for n in names:
         assert f" *   {n}=" in header, n
+
+
+def test_kernel_variant_ids_match_header():
+    """The Python variant names (pin_variant / fused_variant) use the header's WS_KERNEL_* ids,
+    and the library's WS_KERNEL switch accepts every one of them (ws_runtime.cpp)."""
+    hdr = open(os.path.join(ROOT, "include", "ws_hip.h")).read()
+    ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define WS_KERNEL_([A-Z0-9]+) (\d+)", hdr)}
+    assert ids == ws.WeatherSimulation._KERNELS
+    src = open(os.path.join(ROOT, "nvidia-jetson-workload_amd", "csrc", "ws_runtime.cpp")).read()
+    for name in ids:
+        assert f'{{"{name}", ' in src, name
