@@ -168,7 +168,10 @@ struct StepRings {
 // kLag = 2 march bodies behind the producer; an LDS-only workgroup barrier every 2 bodies hands
 // the rows over (the consumer reads rows the producer finished before the last barrier, the
 // producer overwrites slots the consumer finished before it: kU >= 6 ring slots).
-constexpr int kLag = 2;
+#ifndef WS_PC_LAG  // measurement builds: the consumer's lag = the barrier interval, in bodies
+#define WS_PC_LAG 2
+#endif
+constexpr int kLag = WS_PC_LAG;
 
 #ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), fp64 pairs 2
 #define WS_PC_MINW 0
