@@ -40,6 +40,11 @@ VALU_CYCLES = 4        # a wave64 VALU instruction occupies its SIMD16 for 4 cyc
 RAMP_S = 0.4           # untimed sustained load before the timed steps (DVFS clock ramp)
 
 CONFIGS = {
+    # BASELINE configs[0]: the reference's CPU configuration (its example / test size), a smooth
+    # dam-break (h = 10 + 0.5 (1 - tanh((x - W/2) / 8)), u = v = 0; tests/golden/gen_golden.py C1),
+    # measured here on the GPU beside the reference CPU solver on the same workload
+    "c1": dict(W=256, H=256, L=1, model=0, fp64=False, ic="dam_break", dam_width=8.0, cpu_steps_cap=1000,
+               workload="C1: Shallow Water 256x256 smooth dam-break fp32 (the reference's CPU configuration)"),
     "c2": dict(W=4096, H=4096, L=1, model=0, fp64=True, ic="jet_stream",
                workload="C2: Shallow Water 4096x4096 fp64, 1 level"),
     "c3": dict(W=2048, H=2048, L=1, model=1, fp64=False, ic="zonal_flow",
@@ -117,6 +122,14 @@ def host_cores():
     return aff, f"sched_getaffinity: {aff} CPUs"
 
 
+def dam_break_height(W, H, width_cells, dtype):
+    """C1's smooth dam-break height, exactly as tests/golden/gen_golden.py builds it."""
+    import numpy as np
+    x = np.arange(W, dtype=np.float64)
+    row = 10.0 + 0.5 * (1.0 - np.tanh((x - W / 2) / width_cells))
+    return np.broadcast_to(row, (H, W)).astype(dtype)
+
+
 def cpu_baseline(conf, method, budget_s=20.0):
     """Time the reference CPU solver (or the oracle port) on a bounded sample, with one
     OpenMP thread per host core this process may use (host_cores)."""
@@ -129,21 +142,32 @@ def cpu_baseline(conf, method, budget_s=20.0):
         W, H = 4096, 4096  # C5 does not fit host memory in the reference layout: same per-cell work
     # pilot: 1 step to size the sample to ~budget_s
     def run_ref(steps):
+        tmpfiles = []
+        if conf["ic"] == "dam_break":  # a height field, loaded into the reference grid
+            import numpy as np
+            with tempfile.NamedTemporaryFile("wb", suffix=".bin", delete=False) as hf:
+                dam_break_height(W, H, conf["dam_width"], np.float64 if conf["fp64"] else np.float32).tofile(hf)
+            tmpfiles.append(hf.name)
+            ic_lines = ["initialize", f"setfield h {hf.name}"]
+        else:
+            ic_lines = [f"ic {conf['ic']}", "initialize"]
         spec = "\n".join([f"cfg width {W}", f"cfg height {H}", f"cfg model {conf['model']}",
-                          f"cfg method {method}", "cfg max_time 1e30", "create", f"ic {conf['ic']}",
-                          "initialize", "time_run 1", f"time_run {steps}"]) + "\n"
+                          f"cfg method {method}", "cfg max_time 1e30", "create", *ic_lines,
+                          "time_run 1", f"time_run {steps}"]) + "\n"
         with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
             f.write(spec)
+        tmpfiles.append(f.name)
         try:
             out = subprocess.run([ref, f.name], env=env, capture_output=True, text=True, timeout=600).stdout
         finally:
-            os.unlink(f.name)
+            for t in tmpfiles:
+                os.unlink(t)
         secs = [float(l.split()[2]) for l in out.splitlines() if l.startswith("TIME_RUN")]
         return secs[-1]
 
     if os.path.exists(ref):
         pilot = run_ref(1)
-        steps = max(1, min(200, int(budget_s / max(pilot, 1e-6))))
+        steps = max(1, min(conf.get("cpu_steps_cap", 200), int(budget_s / max(pilot, 1e-6))))
         secs = run_ref(steps)
         kind = "reference"
         what = f"reference weather_simulation.cpp (oracle/_ref/ws_ref_{variant}, -O3 -fopenmp)"
@@ -192,6 +216,23 @@ def verdict_over_ranks(dist, ok):
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t[0])
+
+
+def clock_ramp(run_chunk, dist=None, enabled=True):
+    """Untimed sustained load for RAMP_S seconds before the timed steps (the chip raises its
+    clocks over tens of milliseconds of load). Returns the steps run. With more than one rank
+    the stop decision is collective (a MIN over the gloo group after every chunk): each chunk
+    of a slab decomposition is a collective run(), so every rank must run the same number."""
+    steps, t_ramp = 0, time.perf_counter()
+    multi = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    while enabled:
+        go = time.perf_counter() - t_ramp < RAMP_S
+        if multi:
+            go = verdict_over_ranks(dist, go)
+        if not go:
+            break
+        steps += run_chunk()
+    return steps
 
 
 def sum_over_ranks(dist, values):
@@ -301,9 +342,7 @@ def bench_bvort(args, conf, method, world):
     m.set_vorticity(z0)
     if args.warmup > 0:
         m.run(args.warmup)
-    t_ramp = time.perf_counter()  # clock ramp (untimed), as in main()
-    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
-        m.run(2)
+    clock_ramp(lambda: m.run(2) or 2, None, args.warmup > 0)  # one GPU (world 1), as in main()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     m.run(args.steps)
@@ -400,9 +439,7 @@ def bench_lpe(args, conf, method, world):
     m.set_state(*s0)
     if args.warmup > 0:
         m.run(args.warmup)
-    t_ramp = time.perf_counter()  # clock ramp (untimed), as in main()
-    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
-        m.run(2)
+    clock_ramp(lambda: m.run(2) or 2, None, args.warmup > 0)  # one GPU (world 1), as in main()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     m.run(args.steps)
@@ -502,7 +539,8 @@ def main():
     if args.pin:
         k, tb, seg, al = args.pin.split(":")
         sim.pin_variant(kernel=k, steps_per_launch=int(tb), seg_rows=int(seg) or None, align=bool(int(al)))
-    ic = {"jet_stream": ws.JetStreamInitialCondition, "zonal_flow": ws.ZonalFlowInitialCondition}[conf["ic"]]()
+    ic = {"jet_stream": ws.JetStreamInitialCondition, "zonal_flow": ws.ZonalFlowInitialCondition,
+          "dam_break": lambda: None}[conf["ic"]]()  # C1: no IC object (the reset state + the h field)
     # parity self-check before the timed region: the reference's per-slab digests of the C2
     # jet_stream RK4 fp64 case (bitwise, exact numerics) and the default numerics within the
     # north_star tolerance; a failure is reported and the run exits non-zero
@@ -512,8 +550,13 @@ def main():
         parity, parity_detail = self_check(sim, ic, dist if world > 1 else None, rank, world, golden)
         if rank == 0:
             log(f"parity self-check: {parity} {json.dumps(parity_detail)}")
-    sim.set_initial_condition(ic)
+    if ic is not None:
+        sim.set_initial_condition(ic)
     sim.initialize()  # on a slab, the IC is evaluated in global coordinates for the owned rows
+    if conf["ic"] == "dam_break":  # C1: the reference driver's `initialize` + `setfield h` (gen_golden.py)
+        import numpy as np
+        hfull = dam_break_height(conf["W"], conf["H"], conf["dam_width"], np.float64 if conf["fp64"] else np.float32)
+        sim.get_current_grid().set_height_field(np.ascontiguousarray(hfull[sim.row0:sim.row0 + sim.rows]))
 
     def barrier():
         if world > 1:
@@ -525,9 +568,7 @@ def main():
     # load, and W short warm-up steps from idle leave the timed steps on the ramp (measured:
     # C2 0.243 ms per two-step launch warm vs 0.277 when the timed run starts cold). Keep the
     # GPU busy for >= RAMP_S seconds of untimed steps first; reported as ramp_steps.
-    ramp_steps, t_ramp = 0, time.perf_counter()
-    while args.warmup > 0 and time.perf_counter() - t_ramp < RAMP_S:
-        ramp_steps += sim.run(20)
+    ramp_steps = clock_ramp(lambda: sim.run(20), dist if world > 1 else None, args.warmup > 0)
     sim.set_kernel_timing(True, reserve=4 * args.steps + 16)  # events created outside the timed region
     barrier()
     torch.cuda.synchronize()

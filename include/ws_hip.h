@@ -354,8 +354,13 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
 int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows, int32_t* out_cols);
 
 /* Pin (part of) the fused-kernel variant of one simulation; -1 leaves a part to the
- * autotuner. kernel: WS_KERNEL_LDS / _DPPY / _X2Y / _PC / _PC2; steps_per_launch: 1 or 2; seg_rows:
- * output rows per segment; align: 1 = strip output windows on whole 128-byte lines. */
+ * autotuner, which then times only candidates that agree with the pinned parts (a pinned
+ * kernel gets its own best steps per launch, segment length and alignment). kernel:
+ * WS_KERNEL_LDS / _DPPY / _X2Y / _PC / _PC2; steps_per_launch: 1 or 2 (the split variants _PC /
+ * _PC2 advance two steps per launch: 1 is rejected, -1 means 2; _LDS one: 2 is rejected);
+ * seg_rows: output rows per segment; align: 1 = strip output windows on whole 128-byte lines.
+ * The WS_KERNEL / WS_TB / WS_SEG_ROWS environment pins are process-wide and switch tuning off
+ * (what they leave free takes its default; WS_KERNEL=pc|pc2 implies WS_TB=2). */
 #define WS_KERNEL_LDS 0
 #define WS_KERNEL_DPPY 4
 #define WS_KERNEL_X2Y 5

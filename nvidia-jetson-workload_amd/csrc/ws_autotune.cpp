@@ -1,6 +1,7 @@
 // Fused-kernel variant choice and slab schedule choice (internal interfaces: ws_sim.h).
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -26,10 +27,12 @@ static void autotune_time(ws_sim* s) {
     std::vector<Cand> cands;
     const int fixed_seg = s->seg_override;
     const int fixed_tb = s->tb;
+    const int fixed_kernel = s->kernel;
     // two steps per launch only where a run can use them (slab blocks of >= 2 steps)
     const bool tb2_ok = s->block >= 2 || s->nranks == 1;
     for (int k : {kKernDppLdsY, kKernX2Y, kKernPc, kKernPc2, kKernLds})
       for (int tb : {1, 2}) {
+        if (s->kernel_fixed && k != fixed_kernel) continue;  // pinned kernel: tune the rest for it
         if (tb == 2 && (k == kKernLds || !tb2_ok)) continue;
         if (tb == 1 && ws::fused_split(k)) continue;  // a two-step split (its one-step launches are dppy's / x2y's)
         if (s->tb_fixed && k != kKernLds && tb != fixed_tb) continue;
@@ -202,6 +205,12 @@ static TuneKey tune_key(const ws_sim* s) {
     return k;
 }
 
+// The cache file: a version line, then one line of 15 integers per entry (the key, then the
+// choice). Read line by line; a file without the version line (an older build's format), a line
+// with any other field count or a choice out of range is ignored, never read across lines.
+static constexpr const char* kTuneCacheVersion = "ws-tune-cache v2 W H L dtype model nst numerics top bot block "
+                                                 "device kernel seg align tb";
+
 static void tune_file_load_locked() {
     if (g_tune_file_loaded) return;
     g_tune_file_loaded = true;
@@ -209,21 +218,45 @@ static void tune_file_load_locked() {
     if (!path) return;
     FILE* f = std::fopen(path, "r");
     if (!f) return;
-    TuneKey k;
-    TuneChoice c;
-    std::memset(&k, 0, sizeof(k));
-    while (std::fscanf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d %d", &k.W, &k.H, &k.L, &k.dtype, &k.model,
-                       &k.nst, &k.numerics, &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg, &c.align,
-                       &c.tb) == 15)
-        if ((c.kernel == kKernLds || ws::fused_is_dppy(c.kernel)) && (c.tb == 1 || c.tb == 2))
+    char line[512];
+    bool versioned = false;
+    if (std::fgets(line, sizeof line, f)) {
+        line[std::strcspn(line, "\r\n")] = 0;
+        versioned = std::strcmp(line, kTuneCacheVersion) == 0;
+    }
+    while (versioned && std::fgets(line, sizeof line, f)) {
+        TuneKey k;
+        TuneChoice c;
+        std::memset(&k, 0, sizeof(k));
+        int used = 0;
+        const int n = std::sscanf(line, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d %d %n", &k.W, &k.H, &k.L, &k.dtype,
+                                  &k.model, &k.nst, &k.numerics, &k.top, &k.bot, &k.block, &k.device, &c.kernel, &c.seg,
+                                  &c.align, &c.tb, &used);
+        if (n != 15 || line[used] != 0) continue;  // exactly 15 fields
+        const bool kernel_ok = c.kernel == kKernLds || ws::fused_is_dppy(c.kernel);
+        const bool tb_ok = c.tb == 1 || (c.tb == 2 && ws::fused_is_dppy(c.kernel));
+        const bool seg_ok = c.seg > 0 && c.seg <= k.H;
+        if (kernel_ok && tb_ok && seg_ok && (c.align == 0 || c.align == 1) && k.W > 0 && k.H > 0 && k.L > 0)
             g_tune_cache[k] = c;
+    }
     std::fclose(f);
 }
 
 static void tune_file_append_locked(const TuneKey& k, const TuneChoice& c) {
     const char* path = std::getenv("WS_TUNE_CACHE");
     if (!path) return;
-    if (FILE* f = std::fopen(path, "a")) {
+    // a missing, empty or old-format file is (re)started with the version line
+    bool fresh = true;
+    if (FILE* r = std::fopen(path, "r")) {
+        char line[512];
+        if (std::fgets(line, sizeof line, r)) {
+            line[std::strcspn(line, "\r\n")] = 0;
+            fresh = std::strcmp(line, kTuneCacheVersion) != 0;
+        }
+        std::fclose(r);
+    }
+    if (FILE* f = std::fopen(path, fresh ? "w" : "a")) {
+        if (fresh) std::fprintf(f, "%s\n", kTuneCacheVersion);
         std::fprintf(f, "%d %d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", k.W, k.H, k.L, k.dtype, k.model, k.nst,
                      k.numerics, k.top, k.bot, k.block, k.device, c.kernel, c.seg, c.align, c.tb);
         std::fclose(f);
@@ -238,14 +271,14 @@ static void autotune_t(ws_sim* s) {
     s->tuned = true;
     if (!use_fused(s)) return;
     const bool lead = !s->comm || s->comm->rank() == 0;
-    if (lead && !s->kernel_fixed) {
+    if (lead && s->tune_free()) {
         const TuneKey key = tune_key(s);
         bool hit = false;
         {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             tune_file_load_locked();
             auto it = g_tune_cache.find(key);
-            if (it != g_tune_cache.end() && !s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
+            if (it != g_tune_cache.end() && !s->kernel_fixed && !s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
                 s->kernel = it->second.kernel;
                 s->seg_override = it->second.seg;
                 s->align = it->second.align != 0;
@@ -255,7 +288,7 @@ static void autotune_t(ws_sim* s) {
         }
         if (!hit) {
             autotune_time<T>(s);
-            if (!s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
+            if (!s->kernel_fixed && !s->seg_fixed && !s->align_fixed && !s->tb_fixed) {
                 std::lock_guard<std::mutex> lk(g_tune_mu);
                 const TuneChoice c{s->kernel, s->seg_override, s->align ? 1 : 0, s->tb};
                 g_tune_cache[key] = c;

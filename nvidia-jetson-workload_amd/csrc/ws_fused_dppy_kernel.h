@@ -177,6 +177,16 @@ constexpr int kLag = WS_PC_LAG;
 #define WS_PC_MINW 0
 #endif
 constexpr int pc_min_waves(int cpl, int elem) { return WS_PC_MINW > 0 ? WS_PC_MINW : cpl == 2 && elem == 8 ? 2 : 4; }
+
+// Diagnostic builds only (tools/wave_timeline.py, -DWS_WAVE_STAMPS): each workgroup's first lane
+// records its start / end time (100 MHz real-time counter and shader clock), its hardware
+// placement (HW_ID: wave slot, SIMD, CU, SE; XCC id) and work item -- into a buffer no other code
+// reads, via ordinary vector stores. Not part of the product library.
+#ifdef WS_WAVE_STAMPS
+constexpr int kStampWords = 8;
+constexpr int kStampMax = 1 << 16;
+__device__ unsigned long long g_wave_stamps[kStampMax * kStampWords];
+#endif
 template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
 #ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
 #define WS_DPPY_MINW 1
@@ -224,6 +234,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     constexpr auto xslot = [](int gs) { return __builtin_popcount(kXRow & ((1u << (gs - 1)) - 1u)); };
     constexpr int kNX = __builtin_popcount(kXRow);
 
+#ifdef WS_WAVE_STAMPS
+    const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
+#endif
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int strip = w % nstrips;
     int y0, y1;
@@ -552,7 +565,27 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         if (yclamp) march(std::false_type{}, std::true_type{});
         else march(std::false_type{}, std::false_type{});
     }
+#ifdef WS_WAVE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)kStampMax) {
+        const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime(), st_c1 = __builtin_amdgcn_s_memtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID, all 32 bits
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
+        unsigned long long* p = g_wave_stamps + (size_t)blockIdx.x * kStampWords;
+        p[0] = st_r0; p[1] = st_r1; p[2] = st_c0; p[3] = st_c1;
+        p[4] = hw; p[5] = xcc; p[6] = (unsigned long long)w; p[7] = (unsigned long long)(y1 - y0);
+    }
+#endif
 }
+
+#ifdef WS_WAVE_STAMPS
+}  // namespace
+// diagnostic export (built into variant libraries only): copy the stamps of the last launch
+extern "C" int ws_diag_wave_stamps(void* dst, size_t bytes) {
+    if (bytes > sizeof(g_wave_stamps)) bytes = sizeof(g_wave_stamps);
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wave_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+namespace {
+#endif
 
 }  // namespace
 

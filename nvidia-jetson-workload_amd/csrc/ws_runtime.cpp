@@ -143,6 +143,15 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
     require(cfg->grid_width > 0 && cfg->grid_height > 0 && cfg->num_levels > 0, WS_ERR_INVALID,
             "Grid dimensions must be positive");
     require(cfg->dx > 0 && cfg->dy > 0, WS_ERR_INVALID, "Grid spacing must be positive");
+    // The reference runs every backend through its CPU solver (selectOptimalBackend,
+    // weather_simulation.cpp:562-591; the CUDA branch is a placeholder). This library has only
+    // the HIP path: GPU-class backends (CUDA / Hybrid / AdaptiveHybrid) run it, an explicit CPU
+    // backend is refused rather than silently run on the GPU (DESIGN.md deviation D8).
+    require(cfg->compute_backend != WS_BACKEND_CPU, WS_ERR_UNSUPPORTED,
+            "compute_backend CPU: this build has no CPU compute path (only the HIP kernels); use CUDA, "
+            "Hybrid or AdaptiveHybrid");
+    require(cfg->compute_backend >= WS_BACKEND_CUDA && cfg->compute_backend <= WS_BACKEND_ADAPTIVE_HYBRID,
+            WS_ERR_INVALID, "unknown compute_backend");
     set_device(cfg->device_id);
     ws_sim* s = new ws_sim;
     s->cfg = *cfg;
@@ -182,10 +191,14 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
             require(k >= 0, WS_ERR_INVALID, "WS_KERNEL must be x2y, dppy, pc, pc2 or lds");
             s->kernel = k;
             s->kernel_fixed = true;
+            s->kernel_env = true;
+            if (ws::fused_split(k)) s->tb = 2;  // the split variants advance two steps per launch
         }
         if (const char* e = env_str("WS_TB")) {
             s->tb = std::atoi(e);
             require(s->tb == 1 || s->tb == 2, WS_ERR_INVALID, "WS_TB must be 1 or 2");
+            require(!(s->kernel_env && ws::fused_split(s->kernel) && s->tb == 1), WS_ERR_INVALID,
+                    "WS_KERNEL=pc / pc2 advance two steps per launch: WS_TB must be 2 (or unset)");
             s->tb_fixed = true;
         }
         if (const char* e = env_str("WS_SEG_ROWS")) {
@@ -845,7 +858,7 @@ int ws_sim_set_numerics(ws_sim_t* s, int32_t mode) {
         require(s != nullptr, WS_ERR_INVALID, "null sim");
         require(mode == WS_NUMERICS_EXACT || mode == WS_NUMERICS_FAST, WS_ERR_INVALID,
                 "numerics must be WS_NUMERICS_EXACT or WS_NUMERICS_FAST");
-        if (mode != s->numerics && !s->kernel_fixed) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank
+        if (mode != s->numerics && s->tune_free()) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank
         s->numerics = mode;
     });
 }
@@ -869,11 +882,19 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
                 "steps_per_launch must be -1, 1 or 2");
         require(seg_rows == -1 || seg_rows > 0, WS_ERR_INVALID, "seg_rows must be -1 or positive");
         require(align == -1 || align == 0 || align == 1, WS_ERR_INVALID, "align must be -1, 0 or 1");
+        const int k = kernel != -1 ? kernel : s->kernel_fixed ? s->kernel : -1;
+        const int tb = steps_per_launch != -1 ? steps_per_launch : s->tb_fixed ? s->tb : -1;
+        require(!(k != -1 && ws::fused_split(k) && tb == 1), WS_ERR_INVALID,
+                "the split variants (WS_KERNEL_PC, WS_KERNEL_PC2) advance two steps per launch: "
+                "steps_per_launch must be 2 or -1");
+        require(!(k == kKernLds && tb == 2), WS_ERR_INVALID, "WS_KERNEL_LDS advances one step per launch");
         if (kernel != -1) { s->kernel = kernel; s->kernel_fixed = true; }
         if (steps_per_launch != -1) { s->tb = steps_per_launch; s->tb_fixed = true; }
+        else if (k != -1 && ws::fused_split(k)) s->tb = 2;  // the only choice left for a split kernel
         if (seg_rows != -1) { s->seg_override = seg_rows; s->seg_fixed = true; }
         if (align != -1) { s->align = align != 0; s->align_fixed = true; }
-        if (!s->kernel_fixed) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank what is left free
+        // re-rank what is left free, restricted to the pinned parts
+        s->tuned = !s->tune_free() || env_int("WS_AUTOTUNE", 1) == 0;
     });
 }
 

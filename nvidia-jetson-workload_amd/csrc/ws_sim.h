@@ -185,12 +185,16 @@ struct ws_sim {
     int32_t seg_override = 0;    // rows per segment (WS_SEG_ROWS / pin fix it)
     bool align = false;          // strip output windows on whole 128-byte lines (pin fixes it)
     bool kernel_fixed = false, seg_fixed = false, align_fixed = false;
+    bool kernel_env = false;  // WS_KERNEL pins process-wide: no autotuning of what it leaves free
     // time steps per fused launch (temporal blocking; the dppy / x2y kernels): 1, or 2 = two
     // steps per launch inside run(k) (WS_TB / pin fix it, else the autotuner picks)
     int32_t tb = 1;
     bool tb_fixed = false;
     int numerics = WS_NUMERICS_EXACT;  // fused kernels: exact or fast numerics (ws_fused.h)
     bool tuned = false;       // autotune done (first run; WS_AUTOTUNE=0 disables)
+    // whether the autotuner has anything left to choose: parts ws_sim_pin_variant leaves at -1
+    // are tuned (restricted to the pinned parts); a WS_KERNEL environment pin disables tuning
+    bool tune_free() const { return !kernel_env && !(kernel_fixed && seg_fixed && align_fixed && tb_fixed); }
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
     // slab overlap schedule (overlap_block): a block's edge bands run on `edge`, the halo

@@ -145,7 +145,7 @@ int ws_sim_set_slab_schedule(ws_sim_t* s, int32_t block, int32_t overlap) {
             const int thin = s->cfg.grid_height / std::max(1, s->nranks);
             require(block * nst <= std::min(ws::kHalo, thin), WS_ERR_INVALID,
                     "block x stages exceeds the halo rows or the thinnest slab");
-            if (block != s->block && !s->kernel_fixed) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank
+            if (block != s->block && s->tune_free()) s->tuned = env_int("WS_AUTOTUNE", 1) == 0;  // re-rank
             s->block = block;
         }
         s->overlap_mode = overlap;

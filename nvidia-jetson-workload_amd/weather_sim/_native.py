@@ -182,6 +182,8 @@ def check(status):
         raise RuntimeError(msg)  # pybind maps the setters' std::runtime_error to RuntimeError
     if status == WS_ERR_DEVICE:
         raise WsDeviceError(msg)
+    if status == WS_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)  # a RuntimeError subclass: e.g. ComputeBackend.CPU (no CPU path)
     raise RuntimeError(f"ws_hip error {status}: {msg}")
 
 

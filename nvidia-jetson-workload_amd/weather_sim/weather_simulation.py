@@ -8,8 +8,11 @@ MI355X HBM and every step runs as hand-written HIP kernels through libws_hip.so 
 in include/ws_hip.h). There is no CPU compute path and no mock fallback.
 
 Deliberate deviations from the reference (documented in DESIGN.md):
-  * ComputeBackend is accepted and recorded, but every backend runs the HIP path (the
-    reference's CUDA branch was an empty placeholder, weather_simulation.cpp:492-500).
+  * ComputeBackend CUDA / Hybrid / AdaptiveHybrid run the HIP path (the reference runs
+    every backend through its CPU solver; its CUDA branch was an empty placeholder,
+    weather_simulation.cpp:492-500, 562-591). ComputeBackend.CPU (backend="cpu") is refused
+    with NotImplementedError: this build has no CPU compute path, and silently running the
+    GPU under that name would misreport where the work ran.
   * SimulationConfig.double_precision is honoured (fp64 grids); fp32 is the default and
     matches the reference bit-for-bit.
   * num_levels > 1 stores [L, H, W] fields of independent 2-D levels (the reference

@@ -16,7 +16,10 @@ binds: python_bindings.cpp:240-353) and stores inputs and outputs as data:
       (C1 256^2 dam-break 1000 steps; C2-shape 4096^2 fp64 RK4; C3 2048^2 Barotropic;
       C4 per-level 1024^2 PE levels), used by the GPU parity tests at full size.
 
-Usage: python tests/golden/gen_golden.py [--skip-large]
+  --long: only the long-horizon pin of the benched workload (C2 jet_stream 4096^2 fp64 RK4,
+      LONG_STEPS steps), merged into ref_large.json.
+
+Usage: python tests/golden/gen_golden.py [--skip-large | --long]
 """
 import hashlib
 import json
@@ -230,8 +233,37 @@ def large_cases(tmp):
     return out
 
 
+LONG_STEPS = 240  # 40 six-step slab blocks, 120 two-step launches
+
+
+def long_case(tmp):
+    """The benched workload (bench.py c2: jet_stream, RK4, fp64) after LONG_STEPS steps."""
+    out = {}
+    lines = cfg_lines(4096, 4096, SWE, RK4, max_time=1e30) + ["create", ic_line("jet_stream"), "initialize",
+                                                             f"run {LONG_STEPS}", f"snap {tmp}/L.bin"]
+    run_spec("f64", lines, tmp)
+    s = read_snap(f"{tmp}/L.bin")
+    name = f"C2_jet_stream_4096_i2_f64_{LONG_STEPS}"
+    fields = ("u", "v", "h", "vort")
+    out[name] = {"variant": "f64", "step": s["step"], "time": s["time"],
+                 "sha256": {k: digest(s[k]) for k in fields},
+                 "l2": {k: float(np.linalg.norm(s[k].astype(np.float64))) for k in fields},
+                 "spec": [l for l in lines if not l.startswith(("snap", "setfield"))]}
+    print(name, out[name]["step"], out[name]["time"], flush=True)
+    return out
+
+
 def main():
     skip_large = "--skip-large" in sys.argv
+    if "--long" in sys.argv:
+        path = os.path.join(OUT, "ref_large.json")
+        with open(path) as f:
+            large = json.load(f)
+        with tempfile.TemporaryDirectory(prefix="ws_gold_", dir="/tmp") as tmp:
+            large.update(long_case(tmp))
+        with open(path, "w") as f:
+            json.dump(large, f, indent=1, sort_keys=True)
+        return
     with tempfile.TemporaryDirectory(prefix="ws_gold_", dir="/tmp") as tmp:
         for variant in ("f32", "f64"):
             data, meta = small_cases(variant, tmp)

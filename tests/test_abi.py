@@ -112,6 +112,23 @@ def test_physics_models_validate_before_touching_the_device():
         ws.BarotropicVorticityModel({"grid_width": 64})
 
 
+def test_cpu_backend_is_refused_not_silently_run_on_the_gpu():
+    """ComputeBackend.CPU (backend="cpu"): the reference runs it through its CPU solver
+    (weather_simulation.cpp:562-591); this build has only the HIP path, so it refuses the
+    request loudly, before touching any device. GPU-class backends are
+    accepted (they fail here only for want of a device)."""
+    c = ws.SimulationConfig()
+    c.compute_backend = ws.ComputeBackend.CPU
+    with pytest.raises(NotImplementedError, match="no CPU compute path"):
+        ws.WeatherSimulation(c)
+    with pytest.raises(NotImplementedError):
+        ws.WeatherSimulationWrapper(16, 16, backend="cpu")
+    if not _native.is_available():
+        for b in ("cuda", "hybrid", "adaptive"):
+            with pytest.raises(_native.WsDeviceError):
+                ws.WeatherSimulationWrapper(16, 16, backend=b)
+
+
 def test_slab_partition_is_balanced_and_covers_rows():
     for H in (7, 256, 4096, 16384):
         for n in (1, 2, 3, 4, 8):

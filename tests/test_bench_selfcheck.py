@@ -136,3 +136,38 @@ def test_reference_slab_digests_fixture():
             assert set(e["sha256"]) == {"u", "v", "h", "vort"}
     # the whole-grid entry differs from every slab's (distinct data)
     assert len({e["sha256"]["h"] for per in g["slabs"].values() for e in per}) == 1 + 2 + 4 + 8
+
+
+def _ramp_worker(rank, world, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+
+        import bench
+        bench.RAMP_S = 0.15
+        chunks = []
+
+        def chunk():
+            # ranks run at different speeds: each alone would stop after a different count
+            time.sleep(0.004 * (rank + 1))
+            chunks.append(1)
+            return 20
+        steps = bench.clock_ramp(chunk, dist, True)
+        results[rank] = (steps, len(chunks))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_clock_ramp_is_collective(world):
+    """every ramp chunk of a slab decomposition is a collective run(), so the ramp's
+    stop decision must be the same on every rank (a rank stopping one chunk early would leave
+    the others blocked in RCCL)."""
+    with mp.Manager() as m:
+        results = m.dict()
+        mp.spawn(_ramp_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+        res = dict(results)
+    assert len({res[r] for r in range(world)}) == 1, res
+    assert res[0][0] == 20 * res[0][1] and res[0][1] >= 1

@@ -269,6 +269,40 @@ def test_full_size_digests(name, tb, monkeypatch):
                         f"|ref|={ref_l2!r})")
 
 
+LONG_CASE = "C2_jet_stream_4096_i2_f64_240"
+
+
+@pytest.mark.parametrize("kernel", [None, "dppy", "pc", "pc2"])
+def test_long_horizon_benched_workload(kernel, monkeypatch):
+    """The benched workload (bench.py c2: 4096^2 fp64 jet_stream RK4) pinned to the reference
+    over a long horizon (tests/golden/gen_golden.py --long: 240 steps, 120 two-step launches):
+    exact numerics bitwise, and the default fast numerics (what the bench times) within the
+    north_star tolerance of 1e-10 relative L2 per field of that exact (= reference) state.
+    kernel None = the autotuned choice; else a pinned two-step variant."""
+    if kernel:
+        monkeypatch.setenv("WS_KERNEL", kernel)
+        monkeypatch.setenv("WS_TB", "2")
+    d = large_digests()[LONG_CASE]
+    steps = int([l for l in d["spec"] if l.startswith("run ")][0].split()[1])
+    runs = {}
+    for numerics in ("exact", "fast"):
+        sim = make_sim(4096, 4096, 0, 2, True, max_time=1e30)
+        sim.set_numerics(numerics)
+        sim.set_initial_condition(ws.JetStreamInitialCondition())
+        sim.initialize()
+        assert sim.run(steps) == d["step"] == steps
+        g = sim.get_current_grid()
+        u, v = g.get_velocity_field()
+        runs[numerics] = {"u": u, "v": v, "h": g.get_height_field(), "vort": g.get_vorticity_field()}
+        del sim
+    for k, h in d["sha256"].items():
+        assert _digest(runs["exact"][k]) == h, f"{LONG_CASE}: exact {k} differs from the reference"
+    for k in ("u", "v", "h"):
+        ex, fa = runs["exact"][k], runs["fast"][k]
+        rel = float(np.linalg.norm(fa - ex) / np.linalg.norm(ex))
+        assert rel <= 1e-10, f"{LONG_CASE}: fast {k} relative L2 {rel:.3e} > 1e-10"
+
+
 @pytest.mark.parametrize("kernel,tb", [(None, "0"), ("dppy", "2"), ("x2y", "2"), ("pc", "2"), ("pc2", "2")])
 def test_pe_levels_match_reference_per_level(kernel, tb, monkeypatch):
     """C4: PE 1024^2 x 32 levels, level k = jet_stream(strength 10(1+k/32)); each level
