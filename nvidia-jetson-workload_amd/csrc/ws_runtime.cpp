@@ -48,6 +48,8 @@ static void grid_alloc(ws_grid* g, unsigned nfields) {
 void grid_free(ws_grid* g) {
     for (auto& a : g->alloc)
         if (a) { (void)hipFree(a); a = nullptr; }
+    for (auto& e : g->tev)
+        if (e) { (void)hipEventDestroy(e); e = nullptr; }
 }
 
 template <typename T>
@@ -640,6 +642,18 @@ int ws_sim_last_run_stats(const ws_sim_t* s, double* ms, int64_t* launches) {
 }
 
 // ---- KernelAdapter ----
+// The adapter's timing events live on the grid that is timed (created at its first adapter
+// call, destroyed with it): a step costs no event creation.
+static void adapter_events(ws_grid* g) {
+    for (auto& e : g->tev)
+        if (!e) WS_HIP_CHECK(hipEventCreate(&e));
+}
+
+// One explicit-Euler step in -> out (the reference adapter's executeShallowWaterStep: the fused
+// CUDA Euler kernel, shallow_water_kernels.cu:704-719), with the PE T / P update for the
+// primitive-equations entry point. The step runs the fused one-step kernel (fused_dppy, NST = 1,
+// exact numerics: bit-identical to the reference) over the whole grid; widths below two columns
+// take the per-stage kernel.
 static int adapter_step(ws_grid* in, ws_grid* out, double dt, double g, double f, double* ms, bool pe) {
     return guarded([&] {
         require(in && out && in != out, WS_ERR_INVALID, "in and out must be distinct grids");
@@ -647,34 +661,53 @@ static int adapter_step(ws_grid* in, ws_grid* out, double dt, double g, double f
                     in->device == out->device && out->nfields == 8,
                 WS_ERR_SHAPE, "grids must have identical dimensions and precision");
         set_device(in->device);
-        hipEvent_t e0, e1;
-        WS_HIP_CHECK(hipEventCreate(&e0));
-        WS_HIP_CHECK(hipEventCreate(&e1));
+        adapter_events(in);
         auto body = [&](auto tag) {
             using T = decltype(tag);
-            ws::StageArgs<T> a{};
-            a.in_u = (const T*)in->f[0]; a.in_v = (const T*)in->f[1]; a.in_h = (const T*)in->f[2];
-            a.base_u = a.in_u; a.base_v = a.in_v; a.base_h = a.in_h;
-            a.out_u = (T*)out->f[0]; a.out_v = (T*)out->f[1]; a.out_h = (T*)out->f[2];
-            a.c = (T)dt; a.gravity = (T)g; a.coriolis_f = (T)f;
-            a.sp = make_spacing<T>(in->dx, in->dy);
-            WS_HIP_CHECK(ws::launch_stage<T>(ws::kAxpy, a, in->geom(), in->stream));
+            const ws::Geom ge = in->geom();
+            if (in->W >= 2) {
+                ws::FusedArgs<T> a{};
+                a.in_u = (const T*)in->f[0]; a.in_v = (const T*)in->f[1]; a.in_h = (const T*)in->f[2];
+                a.out_u = (T*)out->f[0]; a.out_v = (T*)out->f[1]; a.out_h = (T*)out->f[2];
+                a.c_dt = (T)dt;
+                a.c_half = T(0.5f) * a.c_dt;
+                a.c_dt6 = a.c_dt / T(6.0f);
+                a.gravity = (T)g;
+                a.coriolis_f = (T)f;
+                a.sp1 = a.sp2 = make_spacing<T>(in->dx, in->dy);
+                a.sp_mode = ws::exact_sp_mode(a);
+                a.out_w = ws::fused_out_w(kKernDppLdsY, 1, (int)sizeof(T), false);
+                // segments for ~4 waves per SIMD of the chip (1024 SIMDs), at least 16 rows
+                const int64_t strips = (in->W + a.out_w - 1) / a.out_w;
+                a.seg_rows = (int)std::max<int64_t>(16, (strips * in->H * in->L + 4095) / 4096);
+                a.seg_rows = std::min(a.seg_rows, in->H);
+                a.ga_y0 = 0; a.ga_y1 = in->H; a.ga_n = (in->H + a.seg_rows - 1) / a.seg_rows;
+                a.gb_y0 = a.gb_y1 = 0;
+                a.seg_n = a.ga_n;
+                WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(kKernDppLdsY, 1, 1, a, ge, in->stream));
+            } else {
+                ws::StageArgs<T> a{};
+                a.in_u = (const T*)in->f[0]; a.in_v = (const T*)in->f[1]; a.in_h = (const T*)in->f[2];
+                a.base_u = a.in_u; a.base_v = a.in_v; a.base_h = a.in_h;
+                a.out_u = (T*)out->f[0]; a.out_v = (T*)out->f[1]; a.out_h = (T*)out->f[2];
+                a.c = (T)dt; a.gravity = (T)g; a.coriolis_f = (T)f;
+                a.sp = make_spacing<T>(in->dx, in->dy);
+                WS_HIP_CHECK(ws::launch_stage<T>(ws::kAxpy, a, ge, in->stream));
+            }
             if (pe) {
                 WS_HIP_CHECK(ws::launch_affine<T>((T*)out->f[WS_FIELD_T], (const T*)in->f[WS_FIELD_T], (T)dt,
-                                                  T(288.15f), in->geom(), in->stream));
+                                                  T(288.15f), ge, in->stream));
                 WS_HIP_CHECK(ws::launch_affine<T>((T*)out->f[WS_FIELD_P], (const T*)in->f[WS_FIELD_P], (T)dt,
-                                                  T(1013.25f), in->geom(), in->stream));
+                                                  T(1013.25f), ge, in->stream));
             }
         };
-        WS_HIP_CHECK(hipEventRecord(e0, in->stream));
+        WS_HIP_CHECK(hipEventRecord(in->tev[0], in->stream));
         if (in->dtype == WS_F64) body(double{});
         else body(float{});
-        WS_HIP_CHECK(hipEventRecord(e1, in->stream));
-        WS_HIP_CHECK(hipEventSynchronize(e1));
+        WS_HIP_CHECK(hipEventRecord(in->tev[1], in->stream));
+        WS_HIP_CHECK(hipEventSynchronize(in->tev[1]));
         float t = 0.f;
-        WS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        WS_HIP_CHECK(hipEventElapsedTime(&t, in->tev[0], in->tev[1]));
         out->diag_pending = true;
         if (ms) *ms = t;
     });
@@ -698,18 +731,14 @@ int ws_adapter_calculate_diagnostics(ws_grid_t* g, double* ms) {
     return guarded([&] {
         require(g != nullptr, WS_ERR_INVALID, "null grid");
         set_device(g->device);
-        hipEvent_t e0, e1;
-        WS_HIP_CHECK(hipEventCreate(&e0));
-        WS_HIP_CHECK(hipEventCreate(&e1));
-        WS_HIP_CHECK(hipEventRecord(e0, g->stream));
+        adapter_events(g);
+        WS_HIP_CHECK(hipEventRecord(g->tev[0], g->stream));
         g->diag_pending = true;
         materialize_diag(g);
-        WS_HIP_CHECK(hipEventRecord(e1, g->stream));
-        WS_HIP_CHECK(hipEventSynchronize(e1));
+        WS_HIP_CHECK(hipEventRecord(g->tev[1], g->stream));
+        WS_HIP_CHECK(hipEventSynchronize(g->tev[1]));
         float t = 0.f;
-        WS_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        WS_HIP_CHECK(hipEventElapsedTime(&t, g->tev[0], g->tev[1]));
         if (ms) *ms = t;
     });
 }

@@ -107,6 +107,7 @@ struct ws_grid {
     int32_t top_clamp = 1, bot_clamp = 1;
     int32_t row0 = 0, gH = 0;   // slab: first global row, global height (ICs use global coordinates)
     hipStream_t stream = nullptr;
+    hipEvent_t tev[2] = {};     // timing events of the KernelAdapter entry points (created once)
 
     ws::Geom geom() const {
         ws::Geom g;

@@ -224,6 +224,38 @@ def test_kernel_adapter_step():
     np.testing.assert_array_equal(gout.get_vorticity_field(), s1["vort"])
 
 
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("entry,case", [("execute_shallow_water_step", "step/m0_i0_jet_stream"),
+                                        ("execute_barotropic_step", "step/m1_i0_breaking_wave"),
+                                        ("execute_primitive_equations_step", "step/m2_i0_jet_stream"),
+                                        ("execute_gcm_step", "step/m0_i0_jet_stream")])
+def test_kernel_adapter_entry_points(entry, case, precision):
+    """Every KernelAdapter step entry point (gpu_adaptability.hpp:242-329) against the
+    reference's Euler step of that model (its s0 -> s1 fixture), bitwise in both precisions:
+    u, v, h and the vorticity diagnostic, and for the primitive-equations entry the T / P
+    update with the reference's stale tendencies (+ dt 288.15, + dt 1013.25). The steps run
+    the fused one-step kernel; repeated calls reuse the grid's timing events."""
+    gold = golden(precision)
+    s0, s1 = gold.snap(case, "s0"), gold.snap(case, "s1")
+    H, W = s0["u"].shape
+    a = ws.KernelAdapterFactory.get_instance().get_best_adapter()
+    fp64 = precision == "f64"
+    gin, gout = ws.WeatherGrid(W, H, double_precision=fp64), ws.WeatherGrid(W, H, double_precision=fp64)
+    gin.set_velocity_field(s0["u"], s0["v"])
+    gin.set_height_field(s0["h"])
+    gin.set_pressure_field(s0["p"])
+    gin.set_temperature_field(s0["t"])
+    for _ in range(3):  # the same result every call
+        ms = getattr(a, entry)(gin, gout, 0.01)
+        assert ms >= 0
+        got = state(gout)
+        for k in ("u", "v", "h", "vort"):
+            np.testing.assert_array_equal(got[k], s1[k], err_msg=f"{entry} {precision} {k}")
+        if entry == "execute_primitive_equations_step":
+            np.testing.assert_array_equal(got["t"], s1["t"], err_msg="T drift")
+            np.testing.assert_array_equal(got["p"], s1["p"], err_msg="P drift")
+
+
 def _digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
