@@ -36,7 +36,11 @@ METRIC = "cell-updates/sec + achieved HBM GB/s, SWE 4096^2 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SIMDS = 1024           # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
-VALU_CYCLES = 4        # a wave64 VALU instruction occupies its SIMD16 for 4 cycles (fp64 full rate)
+# issue cycles of one wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md: 32 lanes per
+# cycle, so 2 for 32-bit ops incl. DPP lane moves and packed fp32; fp64 runs at half the fp32
+# rate, 78.6 vs 157.3 TFLOP/s, so 4)
+VALU_CYC_F64 = 4
+VALU_CYC_32 = 2
 RAMP_S = 0.4           # untimed sustained load before the timed steps (DVFS clock ramp)
 
 CONFIGS = {
@@ -594,12 +598,11 @@ def main():
     dev_ms, launches = sim.last_run_stats()
     # dominant kernel = largest total device time
     kind, (n, tot_ms, bpl) = max(stats.items(), key=lambda kv: kv[1][1])
-    achieved = bpl / (tot_ms / n * 1e-3) / 1e9
     step_bytes = sum(b for (_, _, b) in stats.values()) / tb  # one launch per kind covers tb steps
     # PMC of the same variant (tools/profile_round.sh -> profiles/traffic_<config>_<method>.json):
     # HBM bytes and VALU wave-instructions per launch -- used only when the profiled variant
     # (kernel, steps per launch) is the one this run's autotuner chose
-    traffic, valu_insts, traffic_variant = None, None, None
+    traffic, valu_insts, traffic_variant, f64_frac = None, None, None, None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.method}.json")
     if os.path.exists(tfile) and world == 1:
         with open(tfile) as f:
@@ -607,12 +610,18 @@ def main():
         traffic_variant = tj.get("variant")
         if traffic_variant is None or traffic_variant == {"kernel": variant.replace("fused_", ""), "tb": tb}:
             traffic, valu_insts = tj.get(f"kind{kind}"), tj.get("valu_insts")
+            f64_frac = tj.get("valu_f64_frac")
     launch_s = tot_ms / n * 1e-3
-    # compulsory bytes of one launch: y_n read + y_(n+k) written once (6 words per cell, the
-    # k steps in between never leave the chip)
+    # algorithmic bytes of one launch: y_n read + y_(n+k) written once (6 words per cell; the k
+    # steps in between never leave the chip) -- the launch's compulsory HBM traffic
     compulsory = bpl / tb if variant != "stage_kernels" else bpl
-    valu_frac = valu_insts * VALU_CYCLES / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
+    if f64_frac is None:
+        f64_frac = 0.9 if conf["fp64"] else 0.0  # unprofiled: fp64 kernels are ~90 % fp64 VALU
+    valu_cyc = VALU_CYC_F64 * f64_frac + VALU_CYC_32 * (1.0 - f64_frac)
+    valu_frac = valu_insts * valu_cyc / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
     dram_frac = traffic / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
+    binding = None if valu_frac is None or dram_frac is None else "valu" if valu_frac > dram_frac else "hbm"
+    achieved = compulsory / launch_s / 1e9
     result = {
         "metric": METRIC,
         "value": value,
@@ -638,35 +647,39 @@ def main():
                                                    if os.environ.get("WS_SLAB_OVERLAP") is None else
                                                    "fixed by WS_SLAB_OVERLAP"}}
                       if world > 1 else {})},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": binding or "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "frac_kind": "one-step-equivalent: the HBM rate a one-step-per-launch kernel would need "
-                                  "for this cell-update rate (6 words per cell-update); with two steps per "
-                                  "launch it can exceed 1 -- the measured utilisations are compulsory_frac, "
-                                  "dram_frac and valu_frac",
                      "traffic": traffic,
                      "traffic_variant": traffic_variant,
-                     "compulsory_gbs": compulsory / launch_s / 1e9,
-                     "compulsory_frac": compulsory / launch_s / 1e9 / HBM_PEAK_GBS,
                      "kernel": variant if variant != "stage_kernels" else f"stage{kind}",
                      "seg_rows": seg_rows, "strip_out_cols": out_cols, "steps_per_launch": tb,
-                     "bytes_per_launch": bpl, "mean_launch_ms": tot_ms / n,
-                     "byte_model": (f"algorithmic bytes per launch = 6 words per cell-update (read u, v, h + write "
-                                    f"u, v, h: the compulsory traffic of one time step) x {cells} cells x the {tb} "
-                                    f"step(s) one launch advances ({'f64' if conf['fp64'] else 'f32'}); traffic = "
-                                    f"rocprofv3 PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
-                                    f"profiles/traffic_{args.config}_{args.method}.json). A two-step launch reads y_n "
-                                    f"and writes y_(n+2) once, so its traffic is about half its algorithmic bytes: "
-                                    f"dram_gbs is the measured DRAM rate"
+                     "bytes_per_launch": compulsory, "mean_launch_ms": tot_ms / n,
+                     "byte_model": (f"algorithmic bytes per launch = 6 words per cell (read u, v, h of y_n + write "
+                                    f"u, v, h of y_(n+{tb}): the {tb} step(s) in between stay on chip) x {cells} "
+                                    f"cells ({'f64' if conf['fp64'] else 'f32'}); achieved = those bytes / the "
+                                    f"kernel's mean launch time (HIP events on its stream); traffic = rocprofv3 PMC "
+                                    f"HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
+                                    f"profiles/traffic_{args.config}_{args.method}.json), dram_gbs = traffic / the "
+                                    f"same launch time"
                                     if variant != "stage_kernels" else "SURVEY 8(d) stage-kernel words per launch"),
                      "dram_gbs": traffic / launch_s / 1e9 if traffic else None,
                      "dram_frac": dram_frac,
                      "valu_insts_per_launch": valu_insts,
+                     "valu_f64_frac": f64_frac,
                      "valu_frac": valu_frac,
-                     "valu_model": f"SQ_INSTS_VALU (wave64 instructions per launch, PMC) x {VALU_CYCLES} cycles / "
-                                   f"({SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz x mean launch time)",
-                     "binding": (None if valu_frac is None or dram_frac is None
-                                 else "valu" if valu_frac > dram_frac else "hbm")},
+                     "valu_model": f"SQ_INSTS_VALU per launch (PMC) x issue cycles per wave64 instruction on "
+                                   f"SIMD-32 ({VALU_CYC_F64} fp64, {VALU_CYC_32} 32-bit incl. DPP moves; fp64 share "
+                                   f"{f64_frac:.3f} from the profiled kernel) / ({SIMDS} SIMDs x "
+                                   f"{CLOCK_HZ / 1e9:.1f} GHz x mean launch time)",
+                     "binding": binding,
+                     "binding_note": (None if binding is None else
+                                      f"{binding} is the larger measured utilisation; below 0.7 neither HBM nor "
+                                      f"VALU issue saturates (latency / occupancy bound)"
+                                      if max(valu_frac, dram_frac) < 0.7 else f"{binding}-bound"),
+                     "one_step_equivalent_gbs": bpl / launch_s / 1e9,
+                     "one_step_equivalent_note": "6 words per cell-update x cell-updates per launch / launch time: "
+                                                 "the HBM rate a one-step-per-launch kernel would need for this "
+                                                 "cell-update rate (can exceed the peak with two steps per launch)"},
         "achieved_hbm_gbs_step": step_bytes / (dev_ms / args.steps * 1e-3) / 1e9 if dev_ms > 0 else None,
         "cfl": {"value": cfl, "reduction_ms": cfl_ms,
                 "gbs": 3 * (8 if conf["fp64"] else 4) * cells / world / (cfl_ms * 1e-3) / 1e9 if cfl_ms > 0 else None,

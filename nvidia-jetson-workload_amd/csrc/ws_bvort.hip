@@ -78,6 +78,19 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
     const int lx = threadIdx.x + 1;
     const int x = x0 + threadIdx.x;
     if (x >= a.W) return;
+#ifdef WS_BV_ROWREGS
+    // fault investigation build: round 3's per-row register form of the z0 /
+    // accumulator loads, issued together after the barrier
+    T z0v[kTY / kBY], accv[kTY / kBY];
+#pragma unroll
+    for (int r = 0; r < kTY / kBY; ++r) {
+        const int y = y0 + threadIdx.y + r * kBY;
+        if (y >= a.H) break;
+        const int64_t o = (int64_t)y * a.W + x;
+        z0v[r] = a.z0[o];
+        accv[r] = a.acc_mode >= 2 ? a.acc[o] : T(0);
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < kTY / kBY; ++r) {
         const int ly = threadIdx.y + r * kBY + 1;
@@ -96,12 +109,21 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
         k = k - a.beta * ((pe - pw) * a.inv2dx);
         k = k + a.nu * ((ze + zw - T(2) * zc) * a.idx2 + (zn + zs - T(2) * zc) * a.idy2);
         const int64_t o = (int64_t)y * a.W + x;
+#ifdef WS_BV_ROWREGS
+        const T z0 = z0v[r], accr = accv[r];
+#else
         const T z0 = a.z0[o];
+#endif
         switch (a.acc_mode) {
             case 0: a.zout[o] = z0 + a.c * k; break;
             case 1: a.zout[o] = z0 + a.c * k; a.acc[o] = a.w * k; break;
+#ifdef WS_BV_ROWREGS
+            case 2: a.zout[o] = z0 + a.c * k; a.acc[o] = accr + a.w * k; break;
+            default: a.zout[o] = z0 + a.c * (accr + k); break;
+#else
             case 2: a.zout[o] = z0 + a.c * k; a.acc[o] = a.acc[o] + a.w * k; break;
             default: a.zout[o] = z0 + a.c * (a.acc[o] + k); break;
+#endif
         }
     }
 }
@@ -646,6 +668,14 @@ int ws_bvort_create_poisson(const ws_config_t* cfg, int32_t poisson, ws_bvort_t*
             }
             if (f64) ws::upload_eigen<double>(b);
             else ws::upload_eigen<float>(b);
+#ifdef WS_BV_DEBUG
+            // fault investigation build: the model's device allocations, to map a fault address
+            std::fprintf(stderr, "bvort %dx%d %s lds_fft=%d fb=%zu spec=%zu\n", b->W, b->H, f64 ? "f64" : "f32",
+                         (int)b->lds_fft, b->cells() * b->es(), (size_t)nk * b->H * 2 * b->es());
+            const char* names[] = {"z0", "z1", "A", "B", "psi", "acc", "spec", "ax", "ay"};
+            void* ptrs[] = {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay};
+            for (int i = 0; i < 9; ++i) std::fprintf(stderr, "bvort   %s %p\n", names[i], ptrs[i]);
+#endif
         } catch (...) {
             ws::bv_free(b);
             throw;
