@@ -60,8 +60,11 @@ static void autotune_time(ws_sim* s) {
                 const int wave_per_block = k == kKernLds ? 4 : ws::fused_split(k) ? 2 : 1;
                 for (int64_t waves : {1024, 2048, 3072, 4096, 6144})
                     segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
-                if (ws::fused_is_dppy(k))  // more waves per SIMD fit: shorter segments pay
+                if (ws::fused_is_dppy(k)) {  // more waves per SIMD fit: shorter segments pay
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
+                    // the chain schedule: 1 / 2 / 3 rounds of the chip's resident workgroups
+                    for (int r : {1, 2, 3}) segs.push_back(seg_chains(r));
+                }
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
                 for (int seg : segs) cands.push_back({k, seg, al, tb, 0.f});
@@ -130,6 +133,7 @@ static void autotune_time(ws_sim* s) {
         if (best2.size() > 2) best2.resize(2);
         for (const Cand& b : best2)
             for (int d : {-16, -8, 8, 16}) {
+                if (chain_rounds(b.seg) > 0) break;  // a chain schedule has no row neighbours
                 const int seg = b.seg + d;
                 if (seg < 8 || seg > s->slot[0]->H) continue;
                 const bool have = std::any_of(cands.begin(), cands.end(), [&](const Cand& c) {
@@ -235,7 +239,8 @@ static void tune_file_load_locked() {
         if (n != 15 || line[used] != 0) continue;  // exactly 15 fields
         const bool kernel_ok = c.kernel == kKernLds || ws::fused_is_dppy(c.kernel);
         const bool tb_ok = c.tb == 1 || (c.tb == 2 && ws::fused_is_dppy(c.kernel));
-        const bool seg_ok = c.seg > 0 && c.seg <= k.H;
+        const bool seg_ok = (c.seg > 0 && c.seg <= k.H) ||
+                            (ws::fused_is_dppy(c.kernel) && chain_rounds(c.seg) > 0 && chain_rounds(c.seg) <= kMaxChainRounds);
         if (kernel_ok && tb_ok && seg_ok && (c.align == 0 || c.align == 1) && k.W > 0 && k.H > 0 && k.L > 0)
             g_tune_cache[k] = c;
     }

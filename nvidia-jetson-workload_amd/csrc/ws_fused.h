@@ -7,6 +7,12 @@ namespace ws {
 
 constexpr int kFusedCols = 256;  // lanes (= columns) per workgroup strip
 
+// One march of a chain-scheduled launch: output rows [y0, y1) of march column `unit`
+// (= level * strips + strip). See FusedArgs::chains.
+struct ChainSeg {
+    int32_t unit, y0, y1, pad;
+};
+
 template <typename T>
 struct FusedArgs {
     const T *in_u, *in_v, *in_h;  // y_n (rows [-kHalo, H + kHalo) addressable)
@@ -29,6 +35,13 @@ struct FusedArgs {
     int32_t seg_n;
     // spacing / numerics mode of the launch (SpacingMode below), set by the host
     int32_t sp_mode;
+    // Chain schedule (dppy / x2y / pc / pc2; nullptr = the segments above): workgroup w marches
+    // chains[w] -- one long segment per workgroup, sized by the host so that every march of a
+    // round costs the same (edge strips / segments run the dearer clamped code) and a round is
+    // exactly the workgroups the chip holds at once: no round of short-lived waves to quantise,
+    // one warm-up per chain. seg_rows then holds the longest chain's rows.
+    const ChainSeg* chains;
+    int32_t nchains;
 };
 
 // Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).
@@ -98,6 +111,13 @@ hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hip
 // ws_fused_dppypc{,2}_<t>.hip
 template <typename T, int CPL>
 hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs);
+// workgroups of one instantiation one CU holds at once (occupancy; the chain schedule's rounds)
+template <typename T, int NSTEP, int CPL>
+int dppy_blocks_per_cu_tu(int nstages, int sp_mode);
+template <typename T, int CPL>
+int dppy_pc_blocks_per_cu_tu(int nstages, int sp_mode);
+template <typename T>
+int fused_dppy_blocks_per_cu(int variant, int nstages, int nsteps, int sp_mode);
 
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone,
 // rounded up to whole 16-byte DMA chunks for the LDS-DMA variants: a strip's chunks then

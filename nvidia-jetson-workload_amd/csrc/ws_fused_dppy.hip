@@ -18,8 +18,8 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     if (fused_pairs(variant) && (g.pitch % 2 != 0 || g.pitch < g.W + (g.W % 2))) return hipErrorInvalidValue;
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
-    if (nsegs <= 0) return hipSuccess;
-    const int64_t nblocks = (int64_t)nstrips * nsegs * g.L;
+    if (a.chains ? a.nchains <= 0 : nsegs <= 0) return hipSuccess;
+    const int64_t nblocks = a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L;
     if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
     // buffer descriptors span one segment's rows (+ margins); offsets are 32-bit and the
     // dropped-store voffset is 2^31
@@ -36,6 +36,18 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     return nsteps == 1 ? launch_dppy_tu<T, 1, 1>(nstages, a, g, s, nstrips, nsegs)
                        : launch_dppy_tu<T, 2, 1>(nstages, a, g, s, nstrips, nsegs);
 }
+
+template <typename T>
+int fused_dppy_blocks_per_cu(int variant, int nstages, int nsteps, int sp_mode) {
+    if (fused_split(variant) && nsteps == 2)
+        return fused_pairs(variant) ? dppy_pc_blocks_per_cu_tu<T, 2>(nstages, sp_mode)
+                                    : dppy_pc_blocks_per_cu_tu<T, 1>(nstages, sp_mode);
+    if (fused_pairs(variant))
+        return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 2>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 2>(nstages, sp_mode);
+    return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 1>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 1>(nstages, sp_mode);
+}
+template int fused_dppy_blocks_per_cu<float>(int, int, int, int);
+template int fused_dppy_blocks_per_cu<double>(int, int, int, int);
 
 template hipError_t launch_fused_step_dppy<float>(int, int, int, const FusedArgs<float>&, const Geom&, hipStream_t);
 template hipError_t launch_fused_step_dppy<double>(int, int, int, const FusedArgs<double>&, const Geom&, hipStream_t);

@@ -8,4 +8,9 @@ hipError_t launch_dppy_tu(int nstages, const FusedArgs<T>& a, const Geom& g, hip
     return launch_dppy_impl<T, NSTEP, CPL>(nstages, a, g, s, nstrips, nsegs);
 }
 template hipError_t launch_dppy_tu<double, 1, 2>(int, const FusedArgs<double>&, const Geom&, hipStream_t, int, int);
+template <typename T, int NSTEP, int CPL>
+int dppy_blocks_per_cu_tu(int nstages, int sp_mode) {
+    return dppy_blocks_per_cu_impl<T, NSTEP, CPL>(nstages, sp_mode);
+}
+template int dppy_blocks_per_cu_tu<double, 1, 2>(int, int);
 }  // namespace ws

@@ -238,10 +238,18 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
 #endif
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
-    const int strip = w % nstrips;
-    int y0, y1;
-    fused_rows(a, (w / nstrips) % nsegs, y0, y1);
-    const int level = w / (nstrips * nsegs);
+    int strip, y0, y1, level;
+    if (a.chains) {  // chain schedule: this workgroup's march from the host's table
+        const ChainSeg c = a.chains[w];
+        strip = c.unit % nstrips;
+        level = c.unit / nstrips;
+        y0 = c.y0;
+        y1 = c.y1;
+    } else {
+        strip = w % nstrips;
+        fused_rows(a, (w / nstrips) % nsegs, y0, y1);
+        level = w / (nstrips * nsegs);
+    }
 
     const int lane = (int)threadIdx.x % kWave;
     // SPLIT: wave 0 produces the first time step, wave 1 consumes it (wave-uniform)
@@ -599,9 +607,35 @@ constexpr unsigned kLdsPad = WS_DPPY_LDS_PAD;
 constexpr unsigned kLdsPad = 0;
 #endif
 
+// Workgroups of fused_dppy_kernel<T, nstages, NSTEP, mode, CPL, SPLIT> one CU holds at once
+// (the chain schedule's round size is this times the CU count).
+template <typename T, int NSTEP, int CPL, bool SPLIT = false>
+int dppy_blocks_per_cu_impl(int nstages, int sp_mode) {
+    int nb = 0;
+    const int threads = SPLIT ? 2 * kWave : kWave;
+#define WS_DPPY_OCC(N, M)                                                                                            \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>, \
+                                                       threads, kLdsPad)
+#define WS_DPPY_O1(M) WS_DPPY_OCC(1, M)
+#define WS_DPPY_O2(M) WS_DPPY_OCC(2, M)
+#define WS_DPPY_O4(M) WS_DPPY_OCC(4, M)
+    switch (nstages) {
+        case 1: WS_SP_DISPATCH(sp_mode, WS_DPPY_O1) break;
+        case 2: WS_SP_DISPATCH(sp_mode, WS_DPPY_O2) break;
+        case 4: WS_SP_DISPATCH(sp_mode, WS_DPPY_O4) break;
+        default: return 0;
+    }
+#undef WS_DPPY_O1
+#undef WS_DPPY_O2
+#undef WS_DPPY_O4
+#undef WS_DPPY_OCC
+    return nb;
+}
+
 template <typename T, int NSTEP, int CPL, bool SPLIT = false>
 hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
-    const dim3 grid((unsigned)((int64_t)nstrips * nsegs * g.L)), block(SPLIT ? 2 * kWave : kWave);
+    const dim3 grid((unsigned)(a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L)),
+        block(SPLIT ? 2 * kWave : kWave);
 #define WS_DPPY_GO(N, M) \
     hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)
 #define WS_DPPY_G1(M) WS_DPPY_GO(1, M)

@@ -8,4 +8,9 @@ hipError_t launch_dppy_pc_tu(int nstages, const FusedArgs<T>& a, const Geom& g, 
     return launch_dppy_impl<T, 2, CPL, true>(nstages, a, g, s, nstrips, nsegs);
 }
 template hipError_t launch_dppy_pc_tu<float, 1>(int, const FusedArgs<float>&, const Geom&, hipStream_t, int, int);
+template <typename T, int CPL>
+int dppy_pc_blocks_per_cu_tu(int nstages, int sp_mode) {
+    return dppy_blocks_per_cu_impl<T, 2, CPL, true>(nstages, sp_mode);
+}
+template int dppy_pc_blocks_per_cu_tu<float, 1>(int, int);
 }  // namespace ws

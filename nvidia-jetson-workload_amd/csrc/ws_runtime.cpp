@@ -117,7 +117,7 @@ int32_t ws_sim::seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) c
 }
 
 int32_t ws_sim::seg_rows(int nst) const {
-    if (seg_override > 0) return seg_override;
+    if (seg_override > 0 || (wsr::chain_rounds(seg_override) > 0 && kernel != wsr::kKernLds)) return seg_override;
     const int64_t want_blocks = ws::fused_pairs(kernel) ? 2048 : ws::fused_is_dppy(kernel) ? 4096 : 512;
     return seg_for_blocks(nst, want_blocks, 24 * nst);
 }
@@ -133,6 +133,8 @@ void sim_free(ws_sim* s) {
     if (s->edge) (void)hipStreamDestroy(s->edge);
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
     if (s->cfl_scratch) (void)hipFree(s->cfl_scratch);
+    for (auto& t : s->chain_tables)
+        if (t.dev) (void)hipFree(t.dev);
     delete s->comm;
     delete s->staging;
     delete s;
@@ -203,9 +205,11 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
                     "WS_KERNEL=pc / pc2 advance two steps per launch: WS_TB must be 2 (or unset)");
             s->tb_fixed = true;
         }
-        if (const char* e = env_str("WS_SEG_ROWS")) {
+        if (const char* e = env_str("WS_SEG_ROWS")) {  // n > 0 rows, or -2, -3, ...: chain schedule
             s->seg_override = std::atoi(e);
-            s->seg_fixed = s->seg_override > 0;
+            s->seg_fixed = s->seg_override > 0 || (chain_rounds(s->seg_override) > 0 &&
+                                                   chain_rounds(s->seg_override) <= kMaxChainRounds);
+            if (!s->seg_fixed) s->seg_override = 0;
         }
         s->tuned = env_int("WS_AUTOTUNE", 1) == 0;
 
@@ -909,7 +913,8 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
                 "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y, WS_KERNEL_PC or WS_KERNEL_PC2");
         require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2, WS_ERR_INVALID,
                 "steps_per_launch must be -1, 1 or 2");
-        require(seg_rows == -1 || seg_rows > 0, WS_ERR_INVALID, "seg_rows must be -1 or positive");
+        require(seg_rows == -1 || seg_rows > 0 || (chain_rounds(seg_rows) > 0 && chain_rounds(seg_rows) <= kMaxChainRounds),
+                WS_ERR_INVALID, "seg_rows must be -1, positive, or -2 .. -9 (chain schedule of 1 .. 8 rounds)");
         require(align == -1 || align == 0 || align == 1, WS_ERR_INVALID, "align must be -1, 0 or 1");
         const int k = kernel != -1 ? kernel : s->kernel_fixed ? s->kernel : -1;
         const int tb = steps_per_launch != -1 ? steps_per_launch : s->tb_fixed ? s->tb : -1;

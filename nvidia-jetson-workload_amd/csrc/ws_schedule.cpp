@@ -72,12 +72,119 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
     return {g->top_clamp ? 0 : -e, g->bot_clamp ? g->H : g->H + e};
 }
 
-// Launch the fused step kernel over the output rows A U B (segments of seg_rows rows).
+// Chain schedule (ws_fused.h FusedArgs::chains): `rounds` x the workgroups the chip holds at
+// once, each marching ONE chain -- a run of rows of one strip (and level) -- sized so that every
+// chain of a launch costs about the same. A strip whose window touches a global x edge runs the
+// clamped march (kXClampCost x the instructions per row of an interior strip, the fp64 RK4
+// two-step kernel's steady loops: tools/isa_mix.py) and a chain reaching into a global y edge's
+// cone the y-clamped march (kYClampCost), so those get fewer rows. Chains of neighbouring strips
+// at the same rows are adjacent in the table: xcd_work_item() puts them on one XCD (shared halo
+// columns in its L2). Built on first use per launch shape and kept on the device.
+constexpr double kXClampCost = 1.73, kYClampCost = 1.34;
+
+template <typename T>
+static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
+                                             int out_w, int sp_mode) {
+    const ws_grid* g = s->slot[0];
+    const int64_t key[10] = {nst, nsteps, A.y0, A.y1, B.y0, B.y1, rounds, out_w, s->kernel, sp_mode};
+    for (const auto& t : s->chain_tables)
+        if (std::equal(key, key + 10, t.key)) return t;
+    if (s->num_cus == 0) {
+        int cus = 0;
+        WS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
+        s->num_cus = cus;
+    }
+    const int bpc = ws::fused_dppy_blocks_per_cu<T>(s->kernel, nst, nsteps, sp_mode);
+    const int64_t want = (int64_t)rounds * std::max(1, bpc) * std::max(1, s->num_cus);
+    const int cone = nst * nsteps;
+    const int nstrips = (g->W + out_w - 1) / out_w;
+    struct Group {
+        int unit;
+        RowRange r;
+        double wx;  // cost per row of the strip
+        int n = 1;
+        double frac = 0;
+    };
+    std::vector<Group> groups;
+    double total = 0;
+    for (int l = 0; l < g->L; ++l)
+        for (int st = 0; st < nstrips; ++st)
+            for (const RowRange& r : {A, B}) {
+                if (r.rows() <= 0) continue;
+                const bool xc = st == 0 || (st + 1) * out_w >= g->W - cone;  // the kernel's xclamp test
+                Group gr{l * nstrips + st, r, xc ? kXClampCost : 1.0};
+                total += gr.wx * r.rows();
+                groups.push_back(gr);
+            }
+    // chains per group in proportion to its cost (largest remainder), at least one, at most one per row
+    int64_t assigned = 0;
+    for (Group& gr : groups) {
+        const double ideal = (double)want * gr.wx * gr.r.rows() / total;
+        gr.n = (int)std::max(1.0, std::floor(ideal));
+        gr.n = std::min(gr.n, gr.r.rows());
+        gr.frac = ideal - std::floor(ideal);
+        assigned += gr.n;
+    }
+    std::vector<size_t> order(groups.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return groups[x].frac > groups[y].frac; });
+    for (size_t i = 0; assigned < want && i < order.size(); ++i) {
+        Group& gr = groups[order[i]];
+        if (gr.n < gr.r.rows()) { ++gr.n; ++assigned; }
+    }
+    // rows of each group's chains: equal cost, the chains in a y edge's cone priced kYClampCost
+    auto yclamped = [&](int y0, int y1) { return (g->top_clamp && y0 < cone) || (g->bot_clamp && y1 > g->H - cone); };
+    std::vector<std::vector<ws::ChainSeg>> per(groups.size());
+    int maxn = 0;
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        const Group& gr = groups[gi];
+        const int rows = gr.r.rows(), n = gr.n;
+        const bool top = yclamped(gr.r.y0, gr.r.y0 + 1), bot = yclamped(gr.r.y1 - 1, gr.r.y1);
+        // weights of the first / last chain (y-clamped ones are dearer per row)
+        std::vector<double> w(n, 1.0);
+        if (top) w[0] = kYClampCost;
+        if (bot) w[n - 1] = n == 1 ? std::max(w[n - 1], kYClampCost) : kYClampCost;
+        double inv = 0;
+        for (double x : w) inv += 1.0 / x;
+        int y = gr.r.y0;
+        double acc = 0;
+        for (int c = 0; c < n; ++c) {
+            acc += (1.0 / w[c]) / inv * rows;
+            int y1 = c == n - 1 ? gr.r.y1 : gr.r.y0 + (int)std::lround(acc);
+            y1 = std::max(y1, y + 1);
+            y1 = std::min(y1, gr.r.y1 - (n - 1 - c));  // leave a row for every later chain
+            per[gi].push_back(ws::ChainSeg{gr.unit, y, y1, 0});
+            y = y1;
+        }
+        maxn = std::max(maxn, n);
+    }
+    // table order: chain position, then unit -- neighbouring strips at the same rows adjacent
+    ws_sim::ChainTable t;
+    std::copy(key, key + 10, t.key);
+    std::vector<ws::ChainSeg> tab;
+    for (int c = 0; c < maxn; ++c)
+        for (size_t gi = 0; gi < groups.size(); ++gi)
+            if (c < (int)per[gi].size()) {
+                tab.push_back(per[gi][c]);
+                t.max_rows = std::max(t.max_rows, per[gi][c].y1 - per[gi][c].y0);
+            }
+    t.n = (int32_t)tab.size();
+    WS_HIP_CHECK(hipMalloc(&t.dev, tab.size() * sizeof(ws::ChainSeg)));
+    WS_HIP_CHECK(hipMemcpy(t.dev, tab.data(), tab.size() * sizeof(ws::ChainSeg), hipMemcpyHostToDevice));
+    s->chain_tables.push_back(t);
+    return s->chain_tables.back();
+}
+
+// Launch the fused step kernel over the output rows A U B (segments of seg_rows rows, or the
+// chain schedule when seg_rows encodes one: chain_rounds).
 template <typename T>
 void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st, ws_grid* in,
                   ws_grid* out) {
     if (!st) st = s->stream;
-    const int nA = (A.rows() + seg_rows - 1) / seg_rows, nB = (B.rows() + seg_rows - 1) / seg_rows;
+    const int rounds = s->kernel == kKernLds ? 0 : chain_rounds(seg_rows);
+    if (rounds == 0 && seg_rows <= 0) throw WsError(WS_ERR_INVALID, "bad segment rows");
+    const int nA = rounds ? (A.rows() > 0) : (A.rows() + seg_rows - 1) / seg_rows;
+    const int nB = rounds ? (B.rows() > 0) : (B.rows() + seg_rows - 1) / seg_rows;
     if (nA + nB <= 0) return;
     ws_grid* c = in ? in : s->slot[s->cur];    // (the autotuner times launches on other grids)
     ws_grid* n = out ? out : s->slot[1 - s->cur];
@@ -101,6 +208,12 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     // fast = re-associated with FMAs (isotropic spacing; otherwise exact)
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
+    if (rounds) {
+        const ws_sim::ChainTable& t = chain_table<T>(s, nst, nsteps, A, B, rounds, a.out_w, a.sp_mode);
+        a.chains = t.dev;
+        a.nchains = t.n;
+        a.seg_rows = t.max_rows;  // the launcher's descriptor-span check
+    }
     const ws::Geom g = c->geom();
     if (nsteps > 1 && s->kernel == kKernLds) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy, x2y, pc or pc2");
     if (s->kernel == kKernLds) WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st));

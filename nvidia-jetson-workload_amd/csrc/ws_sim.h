@@ -213,6 +213,14 @@ struct ws_sim {
     uint64_t* cfl_scratch = nullptr;     // ws_sim_cfl: per-level partial maxima + results (device)
     int64_t cfl_scratch_n = 0;
     int32_t row0 = 0;
+    // chain-schedule tables (ws_schedule.cpp chain_table), one per launch shape, on the device
+    struct ChainTable {
+        int64_t key[10];
+        ws::ChainSeg* dev = nullptr;
+        int32_t n = 0, max_rows = 0;
+    };
+    std::vector<ChainTable> chain_tables;
+    int32_t num_cus = 0;  // the device's compute units (chain-schedule round size), queried once
 
     // cone = stages per launch (NST x steps per launch): the strip margins
     int out_w(int cone) const { return ws::fused_out_w(kernel, cone, (int)wsr::elem_size(dtype), align); }
@@ -227,6 +235,14 @@ struct ws_sim {
     // warm-up rows stay a small overhead. The autotuner also tries other counts.
     int32_t seg_rows(int nst) const;
 };
+
+namespace wsr {
+// A segment choice (seg_override, ws_sim_pin_variant's seg_rows) of -2, -3, ... selects the chain
+// schedule (ws_fused.h FusedArgs::chains) with 1, 2, ... rounds of the chip's resident workgroups.
+inline int chain_rounds(int seg) { return seg <= -2 ? -seg - 1 : 0; }
+constexpr int seg_chains(int rounds) { return -(rounds + 1); }
+constexpr int kMaxChainRounds = 8;
+}  // namespace wsr
 
 namespace wsr {
 

@@ -266,16 +266,18 @@ def _dam_break(W, H, width_cells, dtype):
     return np.broadcast_to(row, (H, W)).astype(dtype)
 
 
-@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2"])
+@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2", "chain"])
 @pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
                                   "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
                                   "C3_zonal_flow_2048_baro_f32"])
 def test_full_size_digests(name, tb, monkeypatch):
     """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, pc /
     pc2 the producer / consumer split of them (one column / a column pair per lane)."""
-    if tb in ("2", "pc", "pc2"):
-        monkeypatch.setenv("WS_KERNEL", "dppy" if tb == "2" else tb)
+    if tb in ("2", "pc", "pc2", "chain"):
+        monkeypatch.setenv("WS_KERNEL", tb if tb in ("pc", "pc2") else "dppy")
         monkeypatch.setenv("WS_TB", "2")
+    if tb == "chain":  # the chain schedule, one round of the chip's resident waves
+        monkeypatch.setenv("WS_SEG_ROWS", "-2")
     d = large_digests()[name]
     spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
     W, H = int(spec["width"]), int(spec["height"])
@@ -304,16 +306,19 @@ def test_full_size_digests(name, tb, monkeypatch):
 LONG_CASE = "C2_jet_stream_4096_i2_f64_240"
 
 
-@pytest.mark.parametrize("kernel", [None, "dppy", "pc", "pc2"])
+@pytest.mark.parametrize("kernel", [None, "dppy", "pc", "pc2", "dppy-chain"])
 def test_long_horizon_benched_workload(kernel, monkeypatch):
     """The benched workload (bench.py c2: 4096^2 fp64 jet_stream RK4) pinned to the reference
     over a long horizon (tests/golden/gen_golden.py --long: 240 steps, 120 two-step launches):
     exact numerics bitwise, and the default fast numerics (what the bench times) within the
     north_star tolerance of 1e-10 relative L2 per field of that exact (= reference) state.
-    kernel None = the autotuned choice; else a pinned two-step variant."""
+    kernel None = the autotuned choice; else a pinned two-step variant (-chain: on the chain
+    schedule, one round of the chip's resident waves)."""
     if kernel:
-        monkeypatch.setenv("WS_KERNEL", kernel)
+        monkeypatch.setenv("WS_KERNEL", kernel.replace("-chain", ""))
         monkeypatch.setenv("WS_TB", "2")
+        if kernel.endswith("-chain"):
+            monkeypatch.setenv("WS_SEG_ROWS", "-2")
     d = large_digests()[LONG_CASE]
     steps = int([l for l in d["spec"] if l.startswith("run ")][0].split()[1])
     runs = {}
@@ -361,12 +366,14 @@ def test_pe_levels_match_reference_per_level(kernel, tb, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel,tb", FUSED, ids=FUSED_IDS)
-@pytest.mark.parametrize("seg_rows", ["0", "5", "33"])
+@pytest.mark.parametrize("seg_rows", ["0", "5", "33", "-2", "-4"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, tb, monkeypatch):
     """Strip (x) and segment (y) seams of the fused kernel: 700 x 77 grid spans three
-    256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle."""
+    256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle.
+    seg_rows -2 / -4: the chain schedule (1 / 3 rounds of resident workgroups, chains of
+    cost-balanced lengths, y-clamped chains shorter)."""
     from oracle.ws_oracle import OracleSim
 
     monkeypatch.setenv("WS_SEG_ROWS", seg_rows)
