@@ -209,7 +209,13 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
     constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1
     // march unroll: ring slot == phase (SPLIT: >= 6, the handover ring's slots, see above)
-    constexpr int kU = SPLIT ? (6 + kNR - 1) / kNR * kNR : kNR;
+    // SPLIT: between two barriers (every kLag bodies) the consumer reads the rows produced before
+    // the first of them while the producer writes its newest kLag slots, so the handover ring
+    // needs >= 2 kLag + 2 slots, and the barrier intervals must tile the unrolled period
+    constexpr int kHandover = 2 * kLag + 2;
+    constexpr int kUlcm = kNR % kLag == 0 ? kNR : kNR * kLag;  // a multiple of kNR and of kLag (kLag <= 2 divides kNR)
+    constexpr int kU = SPLIT ? (kHandover + kUlcm - 1) / kUlcm * kUlcm : kNR;
+    static_assert(!SPLIT || (kU % kLag == 0 && kU >= 2 * kLag + 2 && kU % kNR == 0), "handover ring vs barrier interval");
     constexpr int kNS = NST * NSTEP;                        // stages per launch (the cone depth)
     // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on (the
     // consumer's bodies lag kLag rows). At most three are peeled: a stage computed before it
