@@ -54,6 +54,23 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
     __shared__ T Z[kTY + 2][kTX + 2];
     const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
     const int tid = threadIdx.y * kTX + threadIdx.x;
+    const int x = x0 + threadIdx.x;
+    const bool xin = x < a.W;
+    // This thread's rows of z0 and of the accumulator, loaded ahead of the tile fill so their
+    // latency overlaps it (indices clamped to a valid cell for threads outside the grid, whose
+    // values are never used). The epilogue below then stores through fixed pointers only: one
+    // zout store per row, the accumulator store under a wave-uniform mode test. (Round 3's
+    // register-array form of these loads ended in a `switch` of stores whose default case --
+    // RK4's final combination -- hipcc compiled to a store through an undefined SGPR pair, an
+    // illegal address at the next row: DESIGN.md §10.)
+    T z0v[kTY / kBY], accv[kTY / kBY];
+#pragma unroll
+    for (int r = 0; r < kTY / kBY; ++r) {
+        const int y = y0 + threadIdx.y + r * kBY;
+        const int64_t o = xin && y < a.H ? (int64_t)y * a.W + x : 0;
+        z0v[r] = a.z0[o];
+        accv[r] = a.acc_mode >= 2 ? a.acc[o] : T(0);
+    }
     // (x0 + lx - 1) lies in [-1, W + kTX], (y0 + ly - 1) in [-1, H + kTY]: one wrap step
     // covers grids at least a tile (+ halo) wide and tall (a wave-uniform test); narrower
     // grids reduce fully (an integer division per element: the fill's dominant VALU cost)
@@ -76,32 +93,18 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
     }
     __syncthreads();
     const int lx = threadIdx.x + 1;
-    const int x = x0 + threadIdx.x;
-    if (x >= a.W) return;
-#ifdef WS_BV_ROWREGS
-    // fault investigation build: round 3's per-row register form of the z0 /
-    // accumulator loads, issued together after the barrier
-    T z0v[kTY / kBY], accv[kTY / kBY];
-#pragma unroll
-    for (int r = 0; r < kTY / kBY; ++r) {
-        const int y = y0 + threadIdx.y + r * kBY;
-        if (y >= a.H) break;
-        const int64_t o = (int64_t)y * a.W + x;
-        z0v[r] = a.z0[o];
-        accv[r] = a.acc_mode >= 2 ? a.acc[o] : T(0);
-    }
-#endif
+    if (!xin) return;
+    const bool keep_acc = a.acc_mode == 1 || a.acc_mode == 2;  // wave-uniform
 #pragma unroll
     for (int r = 0; r < kTY / kBY; ++r) {
         const int ly = threadIdx.y + r * kBY + 1;
         const int y = y0 + ly - 1;
         if (y >= a.H) break;
         // e / w = x +- 1, n / s = y +- 1 (n = the next row in memory, as oracle/bvort_oracle.py)
-        const T pc = P[ly][lx], pe = P[ly][lx + 1], pw = P[ly][lx - 1], pn = P[ly + 1][lx], ps = P[ly - 1][lx];
+        const T pe = P[ly][lx + 1], pw = P[ly][lx - 1], pn = P[ly + 1][lx], ps = P[ly - 1][lx];
         const T pne = P[ly + 1][lx + 1], pnw = P[ly + 1][lx - 1], pse = P[ly - 1][lx + 1], psw = P[ly - 1][lx - 1];
         const T zc = Z[ly][lx], ze = Z[ly][lx + 1], zw = Z[ly][lx - 1], zn = Z[ly + 1][lx], zs = Z[ly - 1][lx];
         const T zne = Z[ly + 1][lx + 1], znw = Z[ly + 1][lx - 1], zse = Z[ly - 1][lx + 1], zsw = Z[ly - 1][lx - 1];
-        (void)pc;
         const T jpp = (pe - pw) * (zn - zs) - (pn - ps) * (ze - zw);
         const T jpx = pe * (zne - zse) - pw * (znw - zsw) - pn * (zne - znw) + ps * (zse - zsw);
         const T jxp = zn * (pne - pnw) - zs * (pse - psw) - ze * (pne - pse) + zw * (pnw - psw);
@@ -109,22 +112,10 @@ __global__ __launch_bounds__(kTX* kBY) void bv_stage_kernel(BvArgs<T> a) {
         k = k - a.beta * ((pe - pw) * a.inv2dx);
         k = k + a.nu * ((ze + zw - T(2) * zc) * a.idx2 + (zn + zs - T(2) * zc) * a.idy2);
         const int64_t o = (int64_t)y * a.W + x;
-#ifdef WS_BV_ROWREGS
-        const T z0 = z0v[r], accr = accv[r];
-#else
-        const T z0 = a.z0[o];
-#endif
-        switch (a.acc_mode) {
-            case 0: a.zout[o] = z0 + a.c * k; break;
-            case 1: a.zout[o] = z0 + a.c * k; a.acc[o] = a.w * k; break;
-#ifdef WS_BV_ROWREGS
-            case 2: a.zout[o] = z0 + a.c * k; a.acc[o] = accr + a.w * k; break;
-            default: a.zout[o] = z0 + a.c * (accr + k); break;
-#else
-            case 2: a.zout[o] = z0 + a.c * k; a.acc[o] = a.acc[o] + a.w * k; break;
-            default: a.zout[o] = z0 + a.c * (a.acc[o] + k); break;
-#endif
-        }
+        // modes 0-2: zout = z0 + c k; 3 (RK4's final): zout = z0 + c (acc + k)
+        a.zout[o] = z0v[r] + a.c * (a.acc_mode == 3 ? accv[r] + k : k);
+        // mode 1: acc = w k; 2: acc += w k
+        if (keep_acc) a.acc[o] = a.acc_mode == 2 ? accv[r] + a.w * k : a.w * k;
     }
 }
 
@@ -668,14 +659,6 @@ int ws_bvort_create_poisson(const ws_config_t* cfg, int32_t poisson, ws_bvort_t*
             }
             if (f64) ws::upload_eigen<double>(b);
             else ws::upload_eigen<float>(b);
-#ifdef WS_BV_DEBUG
-            // fault investigation build: the model's device allocations, to map a fault address
-            std::fprintf(stderr, "bvort %dx%d %s lds_fft=%d fb=%zu spec=%zu\n", b->W, b->H, f64 ? "f64" : "f32",
-                         (int)b->lds_fft, b->cells() * b->es(), (size_t)nk * b->H * 2 * b->es());
-            const char* names[] = {"z0", "z1", "A", "B", "psi", "acc", "spec", "ax", "ay"};
-            void* ptrs[] = {b->z[0], b->z[1], b->A, b->B, b->psi, b->acc, b->spec, b->ax, b->ay};
-            for (int i = 0; i < 9; ++i) std::fprintf(stderr, "bvort   %s %p\n", names[i], ptrs[i]);
-#endif
         } catch (...) {
             ws::bv_free(b);
             throw;

@@ -598,6 +598,12 @@ extern "C" int ws_diag_wave_stamps(void* dst, size_t bytes) {
     if (bytes > sizeof(g_wave_stamps)) bytes = sizeof(g_wave_stamps);
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wave_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
+extern "C" int ws_diag_wave_stamps_reset() {  // zero the records (before the recorded launch)
+    void* p = nullptr;
+    const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_wave_stamps));
+    if (e != hipSuccess) return (int)e;
+    return (int)hipMemset(p, 0, sizeof(g_wave_stamps));
+}
 namespace {
 #endif
 

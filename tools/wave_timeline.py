@@ -36,6 +36,7 @@ args = ap.parse_args()
 conf = bench.CONFIGS[args.config]
 lib = ctypes.CDLL(_native.LIB_PATH)
 lib.ws_diag_wave_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+lib.ws_diag_wave_stamps_reset.argtypes = []
 WORDS, MAXW = 8, 1 << 16
 
 out = {}
@@ -51,7 +52,10 @@ for pin in args.pins.split(","):
     sim.set_initial_condition(ws.JetStreamInitialCondition())
     sim.initialize()
     sim.run(600)  # clocks up
+    sim.synchronize()
+    _native.check(lib.ws_diag_wave_stamps_reset())
     sim.run(2)    # the launch recorded
+    sim.synchronize()
     buf = np.zeros(MAXW * WORDS, dtype=np.uint64)
     _native.check(lib.ws_diag_wave_stamps(buf.ctypes.data, buf.nbytes))
     rec = buf.reshape(MAXW, WORDS)
@@ -83,7 +87,13 @@ for pin in args.pins.split(","):
                mean_life_frac=float(life.mean() / span),
                simd_end_us=[us(float(np.percentile(per_simd_end, p))) for p in (0, 10, 50, 90, 100)],
                occupancy_hist=hist, waves_per_simd_max=int(occ.max()),
-               clock_ghz=float(np.median((rec[:, 3] - rec[:, 2]) / np.maximum(r1 - r0, 1)) / 10.0))
+               clock_ghz=float(np.median((rec[:, 3] - rec[:, 2]) / np.maximum(r1 - r0, 1)) / 10.0),
+               # speed spread of the marches: microseconds per output row of each workgroup
+               us_per_row=[us(float(np.percentile(life / np.maximum(rec[:, 7].astype(np.int64), 1), p)))
+                           for p in (0, 10, 50, 90, 100)],
+               rows=[int(np.percentile(rec[:, 7].astype(np.int64), p)) for p in (0, 50, 100)],
+               xcc_end_us=[us(int(t1[(xcc & 15) == x].max())) if np.any((xcc & 15) == x) else None for x in range(8)],
+               waves_per_simd_at_start=[int(n) for n in np.bincount(np.bincount(inv[t0 < 200]), minlength=4)[:4]])
     out[pin] = res
     print(json.dumps(res), flush=True)
     del sim
