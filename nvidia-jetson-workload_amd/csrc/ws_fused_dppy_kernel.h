@@ -586,7 +586,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
         unsigned long long* p = g_wave_stamps + (size_t)blockIdx.x * kStampWords;
         p[0] = st_r0; p[1] = st_r1; p[2] = st_c0; p[3] = st_c1;
-        p[4] = hw; p[5] = xcc; p[6] = (unsigned long long)w; p[7] = (unsigned long long)(y1 - y0);
+        p[4] = hw; p[5] = xcc;
+        p[6] = (unsigned long long)(unsigned)w | ((unsigned long long)(unsigned)(level * nstrips + strip) << 32);
+        p[7] = (unsigned long long)(unsigned)y0 | ((unsigned long long)(unsigned)y1 << 32);
     }
 #endif
 }

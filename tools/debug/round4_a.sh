@@ -8,4 +8,3 @@ WS_HIP_LIB=$PWD/nvidia-jetson-workload_amd/lib/variants/libws_hip_stamps.so time
 echo "timeline rc=$?"
 timeout -k 10 200 python bench.py --config c1 --method rk4 --steps 1000 --warmup 50 > gpurun_out/c1.json 2> gpurun_out/c1.err
 echo "c1 rc=$?"
-bash tools/debug/bv_fault.sh

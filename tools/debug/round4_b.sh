@@ -9,3 +9,5 @@ rc=$?; echo "bvort tests rc=$rc"; tail -3 gpurun_out/t_bvort.log; [ $rc -eq 0 ] 
 WS_HIP_LIB=$PWD/nvidia-jetson-workload_amd/lib/variants/libws_hip_stamps.so timeout -k 10 300 python tools/wave_timeline.py \
     --pins dppy:2:48:0,dppy:2:-2:0,dppy:2:-3:0,x2y:2:-2:0 --json gpurun_out/timeline_c2b.json > gpurun_out/timeline_c2b.log 2>&1
 echo "timeline rc=$?"
+timeout -k 10 60 tools/issue_probe > gpurun_out/issue_probe.log 2>&1
+echo "probe rc=$?"; cat gpurun_out/issue_probe.log

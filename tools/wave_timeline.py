@@ -72,6 +72,12 @@ for pin in args.pins.split(","):
     span = int(t1.max())
     life = t1 - t0
     us = lambda ticks: ticks / 100.0  # 100 MHz real-time counter
+    unit = (rec[:, 6] >> np.uint64(32)).astype(np.int64)
+    y0_ = (rec[:, 7] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    y1_ = (rec[:, 7] >> np.uint64(32)).astype(np.int64)
+    rows_ = y1_ - y0_
+    q4 = np.minimum(3, (y0_ + y1_) // 2 * 4 // conf["H"])
+    edge = (unit == unit.min()) | (unit == unit.max())
     keys, inv = np.unique(sid, return_inverse=True)
     # time-weighted number of resident waves per SIMD
     grid = np.linspace(0, span, 400)
@@ -89,9 +95,15 @@ for pin in args.pins.split(","):
                occupancy_hist=hist, waves_per_simd_max=int(occ.max()),
                clock_ghz=float(np.median((rec[:, 3] - rec[:, 2]) / np.maximum(r1 - r0, 1)) / 10.0),
                # speed spread of the marches: microseconds per output row of each workgroup
-               us_per_row=[us(float(np.percentile(life / np.maximum(rec[:, 7].astype(np.int64), 1), p)))
-                           for p in (0, 10, 50, 90, 100)],
-               rows=[int(np.percentile(rec[:, 7].astype(np.int64), p)) for p in (0, 50, 100)],
+               us_per_row=[us(float(np.percentile(life / np.maximum(rows_, 1), p))) for p in (0, 10, 50, 90, 100)],
+               rows=[int(np.percentile(rows_, p)) for p in (0, 50, 100)],
+               # per XCD: median us per row, and of the x-clamped strips (first / last)
+               xcc_us_per_row=[round(us(float(np.median((life / np.maximum(rows_, 1))[(xcc & 15) == x]))), 3)
+                               if np.any((xcc & 15) == x) else None for x in range(8)],
+               by_row_quarter_us_per_row=[round(us(float(np.median((life / np.maximum(rows_, 1))[q4 == q]))), 3)
+                                          if np.any(q4 == q) else None for q in range(4)],
+               edge_strip_us_per_row=round(us(float(np.median((life / np.maximum(rows_, 1))[edge]))), 3)
+               if np.any(edge) else None,
                xcc_end_us=[us(int(t1[(xcc & 15) == x].max())) if np.any((xcc & 15) == x) else None for x in range(8)],
                waves_per_simd_at_start=[int(n) for n in np.bincount(np.bincount(inv[t0 < 200]), minlength=4)[:4]])
     out[pin] = res
