@@ -540,17 +540,17 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                 }(), ...);
             }(std::make_integer_sequence<int, kD>{});
         }
-        auto period = [&](auto KWc, auto Ycc, int R) {
+        auto period = [&](auto KWc, int R) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
                 ([&] {
                     constexpr int P = Ps;
                     if constexpr (!SPLIT) {
-                        body(std::integral_constant<int, P>{}, Xc, Ycc, KWc, R + P);
+                        body(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
                     } else {
                         // both waves pass every barrier: the branch is below it
                         if constexpr (P % kLag == 0) lds_barrier();
-                        if constexpr (kProd) pbody(std::integral_constant<int, P>{}, Xc, Ycc, KWc, R + P);
-                        else cbody(std::integral_constant<int, P>{}, Xc, Ycc, KWc, R + P);
+                        if constexpr (kProd) pbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                        else cbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
                     }
                 }(), ...);
             }(std::make_integer_sequence<int, kU>{});
@@ -558,23 +558,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         // warm-up periods (R1 - R0 >= kU: at least the first runs), then the steady march
         [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
             ([&] {
-                if (Ks == 0 || R0 + Ks * kU < R1) period(std::integral_constant<int, Ks>{}, Yc, R0 + Ks * kU);
+                if (Ks == 0 || R0 + Ks * kU < R1) period(std::integral_constant<int, Ks>{}, R0 + Ks * kU);
             }(), ...);
         }(std::make_integer_sequence<int, kNW>{});
-        if constexpr (decltype(Yc)::value) {
-            // A march that reaches a global y edge runs the clamped body only in the periods whose
-            // rows (R - kNS - lag .. R + kU - 1, with a margin) include row 0 or row H - 1: the
-            // rest of a long chain runs the unclamped body (a third fewer instructions). Both
-            // SPLIT waves decide alike (same R), so their barriers still pair up.
-            constexpr int kLo = kNS + (SPLIT ? kLag : 0) + 2;
-            for (int R = R0 + kNW * kU; R < R1; R += kU) {
-                const bool edge = (g.top_clamp && R - kLo <= 0) || (g.bot_clamp && R + kU + 2 >= g.H - 1);
-                if (edge) period(std::integral_constant<int, -1>{}, std::true_type{}, R);
-                else period(std::integral_constant<int, -1>{}, std::false_type{}, R);
-            }
-        } else {
-            for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, Yc, R);
-        }
+        for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     auto march = [&](auto Xc, auto Yc) {

@@ -76,12 +76,11 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
 // once, each marching ONE chain -- a run of rows of one strip (and level) -- sized so that every
 // chain of a launch costs about the same. A strip whose window touches a global x edge runs the
 // clamped march (kXClampCost x the instructions per row of an interior strip, the fp64 RK4
-// two-step kernel's steady loops: tools/isa_mix.py); a chain reaching a global y edge runs the
-// clamped body in its few periods near that edge (kYClampRows extra row-equivalents), so those
-// chains get fewer rows. Chains of neighbouring strips at the same rows are adjacent in the
-// table: xcd_work_item() puts them on one XCD (shared halo columns in its L2). Built on first
-// use per launch shape and kept on the device.
-constexpr double kXClampCost = 1.73, kYClampRows = 8.0;
+// two-step kernel's steady loops: tools/isa_mix.py) and a chain reaching into a global y edge's
+// cone the y-clamped march (kYClampCost), so those get fewer rows. Chains of neighbouring strips
+// at the same rows are adjacent in the table: xcd_work_item() puts them on one XCD (shared halo
+// columns in its L2). Built on first use per launch shape and kept on the device.
+constexpr double kXClampCost = 1.73, kYClampCost = 1.34;
 
 template <typename T>
 static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
@@ -133,22 +132,27 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
         Group& gr = groups[order[i]];
         if (gr.n < gr.r.rows()) { ++gr.n; ++assigned; }
     }
-    // rows of each group's chains: equal cost, the chains at a y edge carrying kYClampRows more
+    // rows of each group's chains: equal cost, the chains in a y edge's cone priced kYClampCost
     auto yclamped = [&](int y0, int y1) { return (g->top_clamp && y0 < cone) || (g->bot_clamp && y1 > g->H - cone); };
     std::vector<std::vector<ws::ChainSeg>> per(groups.size());
     int maxn = 0;
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         const Group& gr = groups[gi];
         const int rows = gr.r.rows(), n = gr.n;
-        const double top = yclamped(gr.r.y0, gr.r.y0 + 1) ? kYClampRows : 0.0;
-        const double bot = yclamped(gr.r.y1 - 1, gr.r.y1) ? kYClampRows : 0.0;
-        const double each = (rows + top + bot) / n;  // cost of one chain, in row-equivalents
+        const bool top = yclamped(gr.r.y0, gr.r.y0 + 1), bot = yclamped(gr.r.y1 - 1, gr.r.y1);
+        // weights of the first / last chain (y-clamped ones are dearer per row)
+        std::vector<double> w(n, 1.0);
+        if (top) w[0] = kYClampCost;
+        if (bot) w[n - 1] = n == 1 ? std::max(w[n - 1], kYClampCost) : kYClampCost;
+        double inv = 0;
+        for (double x : w) inv += 1.0 / x;
         int y = gr.r.y0;
+        double acc = 0;
         for (int c = 0; c < n; ++c) {
-            const double want = each - (c == 0 ? top : 0.0) - (c == n - 1 ? bot : 0.0);
-            int y1 = c == n - 1 ? gr.r.y1 : y + (int)std::lround(std::max(1.0, want));
-            y1 = std::min(y1, gr.r.y1 - (n - 1 - c));  // leave a row for every later chain
+            acc += (1.0 / w[c]) / inv * rows;
+            int y1 = c == n - 1 ? gr.r.y1 : gr.r.y0 + (int)std::lround(acc);
             y1 = std::max(y1, y + 1);
+            y1 = std::min(y1, gr.r.y1 - (n - 1 - c));  // leave a row for every later chain
             per[gi].push_back(ws::ChainSeg{gr.unit, y, y1, 0});
             y = y1;
         }

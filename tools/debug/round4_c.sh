@@ -11,5 +11,3 @@ echo "timeline rc=$?"
 WS_HIP_LIB=$V/libws_hip_stampsrev.so timeout -k 10 300 python tools/wave_timeline.py \
     --pins dppy:2:-2:0 --json gpurun_out/timeline_c2rev.json > gpurun_out/timeline_c2rev.log 2>&1
 echo "timeline rev rc=$?"
-timeout -k 10 300 python tools/pin_timing.py --config c2 --pins auto,dppy:2:56:0,dppy:2:-2:0,dppy:2:-3:0,pc:2:-2:0,pc2:2:-2:0 > gpurun_out/pins_c2c.log 2>&1
-echo "pins rc=$?"; cat gpurun_out/pins_c2c.log
