@@ -55,7 +55,6 @@ struct FusedArgs {
     int32_t nsteal;
     int32_t tail_rows;
     uint32_t epoch;
-    int32_t nthieves;  // thief workgroups launched after the chains' (grid = nchains + nthieves)
 };
 
 // Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).

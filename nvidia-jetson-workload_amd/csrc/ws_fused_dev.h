@@ -184,11 +184,12 @@ __device__ __forceinline__ V3<VT> rk4_final(const V3<VT>& y, T c, const V3<VT>& 
 // XCD-aware work mapping: consecutive work items (neighbouring strips of one segment,
 // which share halo columns) go to blocks b, b+8, ... that the dispatcher places on the
 // same XCD (same L2). Bijective for any block count. Speed only, never correctness.
-__device__ __forceinline__ int xcd_work_item(int nb, int b) {
+__device__ __forceinline__ int xcd_work_item() {
+    const int nb = gridDim.x;
+    const int b = blockIdx.x;
     const int q = nb / 8, rr = nb % 8, xcd = b % 8;
     return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + b / 8;
 }
-__device__ __forceinline__ int xcd_work_item() { return xcd_work_item((int)gridDim.x, (int)blockIdx.x); }
 
 }  // namespace dev
 }  // namespace ws

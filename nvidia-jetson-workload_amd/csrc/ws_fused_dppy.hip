@@ -19,7 +19,7 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     const int nstrips = (g.W + out_w - 1) / out_w;
     const int nsegs = a.seg_n;
     if (a.chains ? a.nchains <= 0 : nsegs <= 0) return hipSuccess;
-    const int64_t nblocks = a.chains ? (int64_t)a.nchains + (a.claim ? a.nthieves : 0) : (int64_t)nstrips * nsegs * g.L;
+    const int64_t nblocks = a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L;
     if (nblocks > 0x7fffffff) return hipErrorInvalidValue;
     // buffer descriptors span one segment's rows (+ margins); offsets are 32-bit and the
     // dropped-store voffset is 2^31

@@ -243,24 +243,39 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
 #ifdef WS_WAVE_STAMPS
     const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
 #endif
+    const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     const int lane = (int)threadIdx.x % kWave;
-    // Work stealing (chain schedule, one-wave variants; FusedArgs::claim): the grid is the
-    // chains' workgroups -- exactly one round of the chip -- followed by thief workgroups, which
-    // the dispatcher places as chain waves finish. A chain wave marches its chain's fixed part,
-    // then continues into the chain's tail items one claim at a time and ends at the first
-    // item a thief holds; a thief takes the first item of the host's steal order (each chain's
-    // last items first) that nobody holds and marches on from it the same way, or exits.
+    // Work stealing (chain schedule, one-wave variants; FusedArgs::claim): a wave marches its
+    // chain's fixed part, then continues into the chain's tail items one claim at a time; once a
+    // claim fails (a thief holds that item) or the chain is done, it steals items in the
+    // host's steal order (each chain's last items first) until none is left.
     const bool steal_on = !SPLIT && a.chains && a.claim;
-    const bool thief = steal_on && (int)blockIdx.x >= a.nchains;
-    // XCD-aware: neighbouring strips share an L2 (owners numbered over the chains' blocks)
-    const int w = xcd_work_item(steal_on ? a.nchains : (int)gridDim.x, thief ? 0 : (int)blockIdx.x);
     int next_item = -1;  // the tail item of this march's chain it may continue into (-1: none)
     int c_tail = 0, c_end = 0, c_nitems = 0, c_item0 = 0;
-    int strip = 0, y0 = 0, y1 = 0, level = 0, yend = 0;  // yend: the last row a continued march may reach
-    bool have = true;
-    if (thief) {
-        have = false;
-        for (;;) {  // the first entry of the steal order whose item nobody holds yet
+    for (int pass = 0;; ++pass) {
+    int strip, y0, y1, level, yend;  // yend: the last row a continued march may reach
+    if (pass == 0) {
+        if (a.chains) {  // chain schedule: this workgroup's march from the host's table
+            const ChainSeg c = a.chains[w];
+            strip = c.unit % nstrips;
+            level = c.unit / nstrips;
+            y0 = c.y0;
+            y1 = c.y1;
+            if (steal_on && c.nitems > 0) {
+                c_tail = c.tail_y0; c_end = c.y1; c_nitems = c.nitems; c_item0 = c.item0;
+                y1 = c_tail;
+                next_item = 0;
+            }
+        } else {
+            strip = w % nstrips;
+            fused_rows(a, (w / nstrips) % nsegs, y0, y1);
+            level = w / (nstrips * nsegs);
+        }
+        yend = next_item >= 0 ? c_end : y1;
+    } else {
+        if (!steal_on) break;
+        int taken = -1;
+        for (;;) {  // the next entry of the steal order whose item nobody holds yet
             uint32_t idx = 0;
             if (lane == 0) idx = __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
@@ -271,36 +286,19 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
             if (lane == 0) old = __hip_atomic_exchange(a.claim + c.item0 + it, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
             if (old != a.epoch) {
+                taken = it;
                 c_tail = c.tail_y0; c_end = c.y1; c_nitems = c.nitems; c_item0 = c.item0;
                 strip = c.unit % nstrips;
                 level = c.unit / nstrips;
-                y0 = c_tail + it * a.tail_rows;
-                y1 = min(y0 + a.tail_rows, c_end);
-                yend = c_end;
-                next_item = it + 1 < c_nitems ? it + 1 : -1;
-                have = true;
                 break;
             }
         }
-    } else if (a.chains) {  // chain schedule: this workgroup's march from the host's table
-        const ChainSeg c = a.chains[w];
-        strip = c.unit % nstrips;
-        level = c.unit / nstrips;
-        y0 = c.y0;
-        y1 = c.y1;
-        if (steal_on && c.nitems > 0) {
-            c_tail = c.tail_y0; c_end = c.y1; c_nitems = c.nitems; c_item0 = c.item0;
-            y1 = c_tail;
-            next_item = 0;
-        }
-        yend = c.y1;
-    } else {
-        strip = w % nstrips;
-        fused_rows(a, (w / nstrips) % nsegs, y0, y1);
-        level = w / (nstrips * nsegs);
-        yend = y1;
+        if (taken < 0) break;
+        y0 = c_tail + taken * a.tail_rows;
+        y1 = min(y0 + a.tail_rows, c_end);
+        yend = c_end;
+        next_item = taken + 1 < c_nitems ? taken + 1 : -1;
     }
-    if (have) {
     // SPLIT: wave 0 produces the first time step, wave 1 consumes it (wave-uniform)
     const bool producer = !SPLIT || __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave) == 0;
     // left margin: the cone (kNS) rounded up to whole 16-byte chunks, so a strip's DMA chunks
@@ -652,7 +650,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         else march(std::false_type{}, std::false_type{});
     }
 #ifdef WS_WAVE_STAMPS
-    if (threadIdx.x == 0 && blockIdx.x < (unsigned)kStampMax) {
+    if (pass == 0 && threadIdx.x == 0 && blockIdx.x < (unsigned)kStampMax) {
         const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime(), st_c1 = __builtin_amdgcn_s_memtime();
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID, all 32 bits
         const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
@@ -663,10 +661,11 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         p[7] = (unsigned long long)(unsigned)y0 | ((unsigned long long)(unsigned)y1 << 32);
     }
 #endif
-    }  // have
+    if (!steal_on) break;
+    }  // passes
     // the last workgroup to finish resets the steal cursor for the next launch on this table
     // (the claims are tagged with the launch's epoch and need no reset)
-    if (steal_on && lane == 0) {
+    if (!SPLIT && a.chains && a.claim && lane == 0) {
         const uint32_t done = __hip_atomic_fetch_add(a.ctl + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (done == gridDim.x - 1) {
             __hip_atomic_store(a.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -730,8 +729,7 @@ int dppy_blocks_per_cu_impl(int nstages, int sp_mode) {
 
 template <typename T, int NSTEP, int CPL, bool SPLIT = false>
 hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, hipStream_t s, int nstrips, int nsegs) {
-    const dim3 grid((unsigned)(a.chains ? (int64_t)a.nchains + (!SPLIT && a.claim ? a.nthieves : 0)
-                                        : (int64_t)nstrips * nsegs * g.L)),
+    const dim3 grid((unsigned)(a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L)),
         block(SPLIT ? 2 * kWave : kWave);
 #define WS_DPPY_GO(N, M) \
     hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)

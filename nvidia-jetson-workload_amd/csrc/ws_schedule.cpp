@@ -264,7 +264,6 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
             a.nsteal = t.nsteal;
             a.tail_rows = t.tail_rows;
             a.epoch = t.epoch;
-            a.nthieves = std::min(t.nsteal, t.n);  // at most one thief per chain slot
         }
     }
     const ws::Geom g = c->geom();
