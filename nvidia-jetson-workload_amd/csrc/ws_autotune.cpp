@@ -64,8 +64,6 @@ static void autotune_time(ws_sim* s) {
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
                     // the chain schedule: 1 / 2 / 3 rounds of the chip's resident workgroups
                     for (int r : {1, 2, 3}) segs.push_back(seg_chains(r));
-                    if (!ws::fused_split(k))  // one-wave variants: chains with work stealing
-                        for (int r : {1, 2}) segs.push_back(seg_chains(r, true));
                 }
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());
@@ -242,7 +240,7 @@ static void tune_file_load_locked() {
         const bool kernel_ok = c.kernel == kKernLds || ws::fused_is_dppy(c.kernel);
         const bool tb_ok = c.tb == 1 || (c.tb == 2 && ws::fused_is_dppy(c.kernel));
         const bool seg_ok = (c.seg > 0 && c.seg <= k.H) ||
-                            (ws::fused_is_dppy(c.kernel) && chain_rounds(c.seg) > 0);
+                            (ws::fused_is_dppy(c.kernel) && chain_rounds(c.seg) > 0 && chain_rounds(c.seg) <= kMaxChainRounds);
         if (kernel_ok && tb_ok && seg_ok && (c.align == 0 || c.align == 1) && k.W > 0 && k.H > 0 && k.L > 0)
             g_tune_cache[k] = c;
     }

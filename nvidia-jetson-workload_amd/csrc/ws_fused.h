@@ -10,10 +10,7 @@ constexpr int kFusedCols = 256;  // lanes (= columns) per workgroup strip
 // One march of a chain-scheduled launch: output rows [y0, y1) of march column `unit`
 // (= level * strips + strip). See FusedArgs::chains.
 struct ChainSeg {
-    int32_t unit, y0, y1;
-    // work stealing: rows [tail_y0, y1) are nitems tail items of FusedArgs::tail_rows rows,
-    // claim ids item0 .. item0 + nitems - 1 (nitems = 0: no tail)
-    int32_t tail_y0, item0, nitems, pad0, pad1;
+    int32_t unit, y0, y1, pad;
 };
 
 template <typename T>
@@ -45,16 +42,6 @@ struct FusedArgs {
     // one warm-up per chain. seg_rows then holds the longest chain's rows.
     const ChainSeg* chains;
     int32_t nchains;
-    // Work stealing over the chains' tails (one-wave variants; nullptr = plain chains): claim
-    // tags of the tail items (== epoch: taken in this launch), the steal cursor (ctl[0]) and the
-    // finished-workgroup count (ctl[16]), the steal order ({chain, item} pairs: every chain's
-    // last item first), this launch's epoch (never 0).
-    uint32_t* claim;
-    uint32_t* ctl;
-    const int32_t* steal;
-    int32_t nsteal;
-    int32_t tail_rows;
-    uint32_t epoch;
 };
 
 // Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).

@@ -244,61 +244,20 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
 #endif
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
-    const int lane = (int)threadIdx.x % kWave;
-    // Work stealing (chain schedule, one-wave variants; FusedArgs::claim): a wave marches its
-    // chain's fixed part, then continues into the chain's tail items one claim at a time; once a
-    // claim fails (a thief holds that item) or the chain is done, it steals items in the
-    // host's steal order (each chain's last items first) until none is left.
-    const bool steal_on = !SPLIT && a.chains && a.claim;
-    int next_item = -1;  // the tail item of this march's chain it may continue into (-1: none)
-    int c_tail = 0, c_end = 0, c_nitems = 0, c_item0 = 0;
-    for (int pass = 0;; ++pass) {
-    int strip, y0, y1, level, yend;  // yend: the last row a continued march may reach
-    if (pass == 0) {
-        if (a.chains) {  // chain schedule: this workgroup's march from the host's table
-            const ChainSeg c = a.chains[w];
-            strip = c.unit % nstrips;
-            level = c.unit / nstrips;
-            y0 = c.y0;
-            y1 = c.y1;
-            if (steal_on && c.nitems > 0) {
-                c_tail = c.tail_y0; c_end = c.y1; c_nitems = c.nitems; c_item0 = c.item0;
-                y1 = c_tail;
-                next_item = 0;
-            }
-        } else {
-            strip = w % nstrips;
-            fused_rows(a, (w / nstrips) % nsegs, y0, y1);
-            level = w / (nstrips * nsegs);
-        }
-        yend = next_item >= 0 ? c_end : y1;
+    int strip, y0, y1, level;
+    if (a.chains) {  // chain schedule: this workgroup's march from the host's table
+        const ChainSeg c = a.chains[w];
+        strip = c.unit % nstrips;
+        level = c.unit / nstrips;
+        y0 = c.y0;
+        y1 = c.y1;
     } else {
-        if (!steal_on) break;
-        int taken = -1;
-        for (;;) {  // the next entry of the steal order whose item nobody holds yet
-            uint32_t idx = 0;
-            if (lane == 0) idx = __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
-            if (idx >= (uint32_t)a.nsteal) break;
-            const int ch = a.steal[2 * idx], it = a.steal[2 * idx + 1];
-            const ChainSeg c = a.chains[ch];
-            uint32_t old = a.epoch;
-            if (lane == 0) old = __hip_atomic_exchange(a.claim + c.item0 + it, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-            if (old != a.epoch) {
-                taken = it;
-                c_tail = c.tail_y0; c_end = c.y1; c_nitems = c.nitems; c_item0 = c.item0;
-                strip = c.unit % nstrips;
-                level = c.unit / nstrips;
-                break;
-            }
-        }
-        if (taken < 0) break;
-        y0 = c_tail + taken * a.tail_rows;
-        y1 = min(y0 + a.tail_rows, c_end);
-        yend = c_end;
-        next_item = taken + 1 < c_nitems ? taken + 1 : -1;
+        strip = w % nstrips;
+        fused_rows(a, (w / nstrips) % nsegs, y0, y1);
+        level = w / (nstrips * nsegs);
     }
+
+    const int lane = (int)threadIdx.x % kWave;
     // SPLIT: wave 0 produces the first time step, wave 1 consumes it (wave-uniform)
     const bool producer = !SPLIT || __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave) == 0;
     // left margin: the cone (kNS) rounded up to whole 16-byte chunks, so a strip's DMA chunks
@@ -323,9 +282,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     const int64_t lofs = (int64_t)level * g.lstride;
     const int rbase = max(y0 - kNS, row_lo);
     // past the last row the march fetches (SPLIT: kLag more bodies, see march)
-    const int rtop = min(row_hi, yend + kNS + (SPLIT ? kLag : 0) + kU + kD + kG);
+    const int rtop = min(row_hi, y1 + kNS + (SPLIT ? kLag : 0) + kU + kD + kG);
     const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
-    const uint32_t out_bytes = (uint32_t)((int64_t)(yend - y0) * g.pitch * sizeof(T));
+    const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
     const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
     const auto ru = make_rsrc(a.in_u + ib, in_bytes), rv = make_rsrc(a.in_v + ib, in_bytes),
                rh = make_rsrc(a.in_h + ib, in_bytes);
@@ -410,7 +369,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
 
     const int R0 = y0 - kNS;
     // rounded up to the unroll (SPLIT: the consumer's bodies lag kLag rows behind the march)
-    int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;  // extended by a continuation
+    const int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
 
     // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
     // stage s computes row Rq - s; the step's output row Rq - NST goes to `out`. Stage s of
@@ -602,36 +561,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                 if (Ks == 0 || R0 + Ks * kU < R1) period(std::integral_constant<int, Ks>{}, R0 + Ks * kU);
             }(), ...);
         }(std::make_integer_sequence<int, kNW>{});
-        // steady march; a stealing wave claims the next tail item of its chain two periods
-        // before the current rows end (the claim's latency hides behind a period) and, if it
-        // got it, extends the march over its rows -- no warm-up, the rings carry on
-        bool asked = false;
-        uint32_t cres = 0;
-        for (int R = R0 + kNW * kU; R < R1; R += kU) {
-            if constexpr (!SPLIT) {
-                if (next_item >= 0) {
-                    const int left = (R1 - R) / kU;
-                    if (!asked && left <= 2) {
-                        cres = a.epoch;
-                        if (lane == 0)
-                            cres = __hip_atomic_exchange(a.claim + c_item0 + next_item, a.epoch, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                        asked = true;
-                    }
-                    if (asked && left <= 1) {
-                        asked = false;
-                        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)cres) != a.epoch) {
-                            y1 = min(c_tail + (next_item + 1) * a.tail_rows, c_end);
-                            R1 = R0 + (y1 + kNS - R0 + kU - 1) / kU * kU;
-                            next_item = next_item + 1 < c_nitems ? next_item + 1 : -1;
-                        } else {
-                            next_item = -1;
-                        }
-                    }
-                }
-            }
-            period(std::integral_constant<int, -1>{}, R);
-        }
+        for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     auto march = [&](auto Xc, auto Yc) {
@@ -641,7 +571,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     };
     // global edges matter only to strips / segments within kNS cells of them
     const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - kNS;
-    const bool yclamp = (g.top_clamp && y0 < kNS) || (g.bot_clamp && yend > g.H - kNS);
+    const bool yclamp = (g.top_clamp && y0 < kNS) || (g.bot_clamp && y1 > g.H - kNS);
     if (xclamp) {
         if (yclamp) march(std::true_type{}, std::true_type{});
         else march(std::true_type{}, std::false_type{});
@@ -650,7 +580,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         else march(std::false_type{}, std::false_type{});
     }
 #ifdef WS_WAVE_STAMPS
-    if (pass == 0 && threadIdx.x == 0 && blockIdx.x < (unsigned)kStampMax) {
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)kStampMax) {
         const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime(), st_c1 = __builtin_amdgcn_s_memtime();
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID, all 32 bits
         const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
@@ -661,17 +591,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         p[7] = (unsigned long long)(unsigned)y0 | ((unsigned long long)(unsigned)y1 << 32);
     }
 #endif
-    if (!steal_on) break;
-    }  // passes
-    // the last workgroup to finish resets the steal cursor for the next launch on this table
-    // (the claims are tagged with the launch's epoch and need no reset)
-    if (!SPLIT && a.chains && a.claim && lane == 0) {
-        const uint32_t done = __hip_atomic_fetch_add(a.ctl + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == gridDim.x - 1) {
-            __hip_atomic_store(a.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.ctl + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 #ifdef WS_WAVE_STAMPS

@@ -134,8 +134,7 @@ void sim_free(ws_sim* s) {
     if (s->stream && s->own_stream) (void)hipStreamDestroy(s->stream);
     if (s->cfl_scratch) (void)hipFree(s->cfl_scratch);
     for (auto& t : s->chain_tables)
-        for (void* q : {(void*)t.dev, (void*)t.claim, (void*)t.ctl, (void*)t.steal})
-            if (q) (void)hipFree(q);
+        if (t.dev) (void)hipFree(t.dev);
     delete s->comm;
     delete s->staging;
     delete s;
@@ -208,7 +207,8 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         }
         if (const char* e = env_str("WS_SEG_ROWS")) {  // n > 0 rows, or -2, -3, ...: chain schedule
             s->seg_override = std::atoi(e);
-            s->seg_fixed = s->seg_override > 0 || chain_rounds(s->seg_override) > 0;
+            s->seg_fixed = s->seg_override > 0 || (chain_rounds(s->seg_override) > 0 &&
+                                                   chain_rounds(s->seg_override) <= kMaxChainRounds);
             if (!s->seg_fixed) s->seg_override = 0;
         }
         s->tuned = env_int("WS_AUTOTUNE", 1) == 0;
@@ -913,9 +913,8 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
                 "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y, WS_KERNEL_PC or WS_KERNEL_PC2");
         require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2, WS_ERR_INVALID,
                 "steps_per_launch must be -1, 1 or 2");
-        require(seg_rows == -1 || seg_rows > 0 || chain_rounds(seg_rows) > 0, WS_ERR_INVALID,
-                "seg_rows must be -1, positive, -2 .. -9 (chain schedule of 1 .. 8 rounds) or -12 .. -19 (the same "
-                "with work stealing)");
+        require(seg_rows == -1 || seg_rows > 0 || (chain_rounds(seg_rows) > 0 && chain_rounds(seg_rows) <= kMaxChainRounds),
+                WS_ERR_INVALID, "seg_rows must be -1, positive, or -2 .. -9 (chain schedule of 1 .. 8 rounds)");
         require(align == -1 || align == 0 || align == 1, WS_ERR_INVALID, "align must be -1, 0 or 1");
         const int k = kernel != -1 ? kernel : s->kernel_fixed ? s->kernel : -1;
         const int tb = steps_per_launch != -1 ? steps_per_launch : s->tb_fixed ? s->tb : -1;

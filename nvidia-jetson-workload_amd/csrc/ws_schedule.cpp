@@ -82,22 +82,13 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
 // columns in its L2). Built on first use per launch shape and kept on the device.
 constexpr double kXClampCost = 1.73, kYClampCost = 1.34;
 
-// Work stealing over the chains (chain_steal): the last kTailFrac of every chain's rows are
-// tail items of kTailRows rows. The owner marches on into them one claim at a time; a wave
-// that is done steals items in the steal order -- every chain's last item first, then the
-// next-to-last, ... -- so owner and thieves meet as late as possible, and a chip whose XCDs run
-// at different speeds (measured: two of eight ~15 % slower on the chain schedule,
-// tools/wave_timeline.py) still ends its launch together.
-constexpr double kTailFrac = 0.3;
-constexpr int kTailRows = 24;
-
 template <typename T>
-static ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
-                                       bool steal, int out_w, int sp_mode, hipStream_t st) {
+static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
+                                             int out_w, int sp_mode) {
     const ws_grid* g = s->slot[0];
-    const int64_t key[11] = {nst, nsteps, A.y0, A.y1, B.y0, B.y1, rounds, out_w, s->kernel, sp_mode, steal};
-    for (auto& t : s->chain_tables)
-        if (std::equal(key, key + 11, t.key)) return t;
+    const int64_t key[10] = {nst, nsteps, A.y0, A.y1, B.y0, B.y1, rounds, out_w, s->kernel, sp_mode};
+    for (const auto& t : s->chain_tables)
+        if (std::equal(key, key + 10, t.key)) return t;
     if (s->num_cus == 0) {
         int cus = 0;
         WS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
@@ -162,14 +153,14 @@ static ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange 
             int y1 = c == n - 1 ? gr.r.y1 : gr.r.y0 + (int)std::lround(acc);
             y1 = std::max(y1, y + 1);
             y1 = std::min(y1, gr.r.y1 - (n - 1 - c));  // leave a row for every later chain
-            per[gi].push_back(ws::ChainSeg{gr.unit, y, y1, y1, 0, 0, 0, 0});
+            per[gi].push_back(ws::ChainSeg{gr.unit, y, y1, 0});
             y = y1;
         }
         maxn = std::max(maxn, n);
     }
     // table order: chain position, then unit -- neighbouring strips at the same rows adjacent
     ws_sim::ChainTable t;
-    std::copy(key, key + 11, t.key);
+    std::copy(key, key + 10, t.key);
     std::vector<ws::ChainSeg> tab;
     for (int c = 0; c < maxn; ++c)
         for (size_t gi = 0; gi < groups.size(); ++gi)
@@ -177,36 +168,6 @@ static ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange 
                 tab.push_back(per[gi][c]);
                 t.max_rows = std::max(t.max_rows, per[gi][c].y1 - per[gi][c].y0);
             }
-    std::vector<int32_t> sorder;  // steal order: {chain, item} pairs
-    if (steal) {
-        int32_t items = 0, maxk = 0;
-        for (ws::ChainSeg& c : tab) {
-            const int rows = c.y1 - c.y0;
-            const int k = (int)std::floor(rows * kTailFrac / kTailRows);
-            if (k < 1 || rows - k * kTailRows < 2 * cone) continue;  // too short to split
-            c.tail_y0 = c.y1 - k * kTailRows;
-            c.item0 = items;
-            c.nitems = k;
-            items += k;
-            maxk = std::max(maxk, k);
-        }
-        for (int d = 0; d < maxk; ++d)  // every chain's last item, then the next-to-last, ...
-            for (size_t ci = 0; ci < tab.size(); ++ci)
-                if (d < tab[ci].nitems) {
-                    sorder.push_back((int32_t)ci);
-                    sorder.push_back(tab[ci].nitems - 1 - d);
-                }
-        t.nsteal = (int32_t)(sorder.size() / 2);
-        t.tail_rows = kTailRows;
-        WS_HIP_CHECK(hipMalloc(&t.claim, std::max<int32_t>(1, items) * sizeof(uint32_t)));
-        // zeroed on the launch's stream (a legacy-stream hipMemset is not ordered with it)
-        WS_HIP_CHECK(hipMemsetAsync(t.claim, 0, std::max<int32_t>(1, items) * sizeof(uint32_t), st));
-        WS_HIP_CHECK(hipMalloc(&t.ctl, 32 * sizeof(uint32_t)));
-        WS_HIP_CHECK(hipMemsetAsync(t.ctl, 0, 32 * sizeof(uint32_t), st));
-        WS_HIP_CHECK(hipMalloc(&t.steal, std::max<size_t>(2, sorder.size()) * sizeof(int32_t)));
-        if (!sorder.empty())
-            WS_HIP_CHECK(hipMemcpy(t.steal, sorder.data(), sorder.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    }
 #ifdef WS_CHAIN_REVERSE  // measurement builds: the table in reverse order (bottom rows on the first XCDs)
     std::reverse(tab.begin(), tab.end());
 #endif
@@ -224,7 +185,6 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
                   ws_grid* out) {
     if (!st) st = s->stream;
     const int rounds = s->kernel == kKernLds ? 0 : chain_rounds(seg_rows);
-    const bool steal = rounds > 0 && chain_steal(seg_rows) && !ws::fused_split(s->kernel);
     if (rounds == 0 && seg_rows <= 0) throw WsError(WS_ERR_INVALID, "bad segment rows");
     const int nA = rounds ? (A.rows() > 0) : (A.rows() + seg_rows - 1) / seg_rows;
     const int nB = rounds ? (B.rows() > 0) : (B.rows() + seg_rows - 1) / seg_rows;
@@ -252,19 +212,10 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
     if (rounds) {
-        ws_sim::ChainTable& t = chain_table<T>(s, nst, nsteps, A, B, rounds, steal, a.out_w, a.sp_mode, st);
+        const ws_sim::ChainTable& t = chain_table<T>(s, nst, nsteps, A, B, rounds, a.out_w, a.sp_mode);
         a.chains = t.dev;
         a.nchains = t.n;
         a.seg_rows = t.max_rows;  // the launcher's descriptor-span check
-        if (steal && t.nsteal > 0) {
-            if (++t.epoch == 0) ++t.epoch;  // claim tags of this launch (0 = never claimed)
-            a.claim = t.claim;
-            a.ctl = t.ctl;
-            a.steal = t.steal;
-            a.nsteal = t.nsteal;
-            a.tail_rows = t.tail_rows;
-            a.epoch = t.epoch;
-        }
     }
     const ws::Geom g = c->geom();
     if (nsteps > 1 && s->kernel == kKernLds) throw WsError(WS_ERR_INVALID, "multi-step launch needs dppy, x2y, pc or pc2");

@@ -215,15 +215,9 @@ struct ws_sim {
     int32_t row0 = 0;
     // chain-schedule tables (ws_schedule.cpp chain_table), one per launch shape, on the device
     struct ChainTable {
-        int64_t key[11];
+        int64_t key[10];
         ws::ChainSeg* dev = nullptr;
         int32_t n = 0, max_rows = 0;
-        // work stealing (chain_steal): claim tags, cursor / done counters, steal order
-        uint32_t* claim = nullptr;
-        uint32_t* ctl = nullptr;
-        int32_t* steal = nullptr;
-        int32_t nsteal = 0, tail_rows = 0;
-        uint32_t epoch = 0;
     };
     std::vector<ChainTable> chain_tables;
     int32_t num_cus = 0;  // the device's compute units (chain-schedule round size), queried once
@@ -243,17 +237,11 @@ struct ws_sim {
 };
 
 namespace wsr {
-// A segment choice (seg_override, ws_sim_pin_variant's seg_rows) of -2 .. -9 selects the chain
-// schedule (ws_fused.h FusedArgs::chains) with 1 .. 8 rounds of the chip's resident workgroups;
-// -12 .. -19 the same with work stealing over the chains' tails (one-wave variants).
+// A segment choice (seg_override, ws_sim_pin_variant's seg_rows) of -2, -3, ... selects the chain
+// schedule (ws_fused.h FusedArgs::chains) with 1, 2, ... rounds of the chip's resident workgroups.
+inline int chain_rounds(int seg) { return seg <= -2 ? -seg - 1 : 0; }
+constexpr int seg_chains(int rounds) { return -(rounds + 1); }
 constexpr int kMaxChainRounds = 8;
-inline int chain_rounds(int seg) {
-    if (seg <= -2 && seg >= -(kMaxChainRounds + 1)) return -seg - 1;
-    if (seg <= -12 && seg >= -(kMaxChainRounds + 11)) return -seg - 11;
-    return 0;
-}
-inline bool chain_steal(int seg) { return seg <= -12 && seg >= -(kMaxChainRounds + 11); }
-constexpr int seg_chains(int rounds, bool steal = false) { return steal ? -(rounds + 11) : -(rounds + 1); }
 }  // namespace wsr
 
 namespace wsr {

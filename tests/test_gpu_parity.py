@@ -266,18 +266,18 @@ def _dam_break(W, H, width_cells, dtype):
     return np.broadcast_to(row, (H, W)).astype(dtype)
 
 
-@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2", "chain", "steal"])
+@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2", "chain"])
 @pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
                                   "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
                                   "C3_zonal_flow_2048_baro_f32"])
 def test_full_size_digests(name, tb, monkeypatch):
     """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, pc /
     pc2 the producer / consumer split of them (one column / a column pair per lane)."""
-    if tb in ("2", "pc", "pc2", "chain", "steal"):
+    if tb in ("2", "pc", "pc2", "chain"):
         monkeypatch.setenv("WS_KERNEL", tb if tb in ("pc", "pc2") else "dppy")
         monkeypatch.setenv("WS_TB", "2")
-    if tb in ("chain", "steal"):  # the chain schedule, one round of the chip's resident waves
-        monkeypatch.setenv("WS_SEG_ROWS", "-2" if tb == "chain" else "-12")
+    if tb == "chain":  # the chain schedule, one round of the chip's resident waves
+        monkeypatch.setenv("WS_SEG_ROWS", "-2")
     d = large_digests()[name]
     spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
     W, H = int(spec["width"]), int(spec["height"])
@@ -306,7 +306,7 @@ def test_full_size_digests(name, tb, monkeypatch):
 LONG_CASE = "C2_jet_stream_4096_i2_f64_240"
 
 
-@pytest.mark.parametrize("kernel", [None, "dppy", "pc", "pc2", "dppy-chain", "dppy-steal", "x2y-steal"])
+@pytest.mark.parametrize("kernel", [None, "dppy", "pc", "pc2", "dppy-chain"])
 def test_long_horizon_benched_workload(kernel, monkeypatch):
     """The benched workload (bench.py c2: 4096^2 fp64 jet_stream RK4) pinned to the reference
     over a long horizon (tests/golden/gen_golden.py --long: 240 steps, 120 two-step launches):
@@ -315,12 +315,10 @@ def test_long_horizon_benched_workload(kernel, monkeypatch):
     kernel None = the autotuned choice; else a pinned two-step variant (-chain: on the chain
     schedule, one round of the chip's resident waves)."""
     if kernel:
-        monkeypatch.setenv("WS_KERNEL", kernel.split("-")[0])
+        monkeypatch.setenv("WS_KERNEL", kernel.replace("-chain", ""))
         monkeypatch.setenv("WS_TB", "2")
         if kernel.endswith("-chain"):
             monkeypatch.setenv("WS_SEG_ROWS", "-2")
-        if kernel.endswith("-steal"):  # chains with work stealing over their tails
-            monkeypatch.setenv("WS_SEG_ROWS", "-12")
     d = large_digests()[LONG_CASE]
     steps = int([l for l in d["spec"] if l.startswith("run ")][0].split()[1])
     runs = {}
@@ -368,7 +366,7 @@ def test_pe_levels_match_reference_per_level(kernel, tb, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel,tb", FUSED, ids=FUSED_IDS)
-@pytest.mark.parametrize("seg_rows", ["0", "5", "33", "-2", "-4", "-12"])
+@pytest.mark.parametrize("seg_rows", ["0", "5", "33", "-2", "-4"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, tb, monkeypatch):
