@@ -36,11 +36,12 @@ METRIC = "cell-updates/sec + achieved HBM GB/s, SWE 4096^2 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SIMDS = 1024           # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
-# issue cycles of one wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md: 32 lanes per
-# cycle, so 2 for 32-bit ops incl. DPP lane moves and packed fp32; fp64 runs at half the fp32
-# rate, 78.6 vs 157.3 TFLOP/s, so 4)
-VALU_CYC_F64 = 4
-VALU_CYC_32 = 2
+# issue cycles of one wave64 VALU instruction on a SIMD-32 at saturation: 2 (32 lanes per cycle,
+# MI355X_MICROARCH.md). Measured on this chip for fp64 too (tools/issue_probe.hip,
+# profiles/r04_issue_probe.txt): independent v_fma_f64 streams cost 5.2 / 3.5 / 3.0 / 2.4 SIMD
+# cycles per instruction at 1 / 2 / 3 / 4 waves per SIMD, DPP moves 4.4 / 3.2 / 2.8 / 2.6 -- fp64
+# is not half rate here, and the fused kernels' limit is issue latency at their occupancy.
+VALU_CYC = 2
 RAMP_S = 0.4           # untimed sustained load before the timed steps (DVFS clock ramp)
 
 CONFIGS = {
@@ -615,10 +616,7 @@ def main():
     # algorithmic bytes of one launch: y_n read + y_(n+k) written once (6 words per cell; the k
     # steps in between never leave the chip) -- the launch's compulsory HBM traffic
     compulsory = bpl / tb if variant != "stage_kernels" else bpl
-    if f64_frac is None:
-        f64_frac = 0.9 if conf["fp64"] else 0.0  # unprofiled: fp64 kernels are ~90 % fp64 VALU
-    valu_cyc = VALU_CYC_F64 * f64_frac + VALU_CYC_32 * (1.0 - f64_frac)
-    valu_frac = valu_insts * valu_cyc / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
+    valu_frac = valu_insts * VALU_CYC / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
     dram_frac = traffic / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
     binding = None if valu_frac is None or dram_frac is None else "valu" if valu_frac > dram_frac else "hbm"
     achieved = compulsory / launch_s / 1e9
@@ -667,10 +665,10 @@ def main():
                      "valu_insts_per_launch": valu_insts,
                      "valu_f64_frac": f64_frac,
                      "valu_frac": valu_frac,
-                     "valu_model": f"SQ_INSTS_VALU per launch (PMC) x issue cycles per wave64 instruction on "
-                                   f"SIMD-32 ({VALU_CYC_F64} fp64, {VALU_CYC_32} 32-bit incl. DPP moves; fp64 share "
-                                   f"{f64_frac:.3f} from the profiled kernel) / ({SIMDS} SIMDs x "
-                                   f"{CLOCK_HZ / 1e9:.1f} GHz x mean launch time)",
+                     "valu_model": f"SQ_INSTS_VALU per launch (PMC) x {VALU_CYC} issue cycles per wave64 "
+                                   f"instruction on SIMD-32 (fp64 included: measured, tools/issue_probe.hip) / "
+                                   f"({SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz x mean launch time); valu_f64_frac = "
+                                   f"the fp64 share (PMC SQ_INSTS_VALU_{{ADD,MUL,FMA,TRANS}}_F64)",
                      "binding": binding,
                      "binding_note": (None if binding is None else
                                       f"{binding} is the larger measured utilisation; below 0.7 neither HBM nor "
