@@ -640,8 +640,8 @@ def main():
                    **({"slab_schedule": {"steps_per_exchange": block,
                                          "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap],
                                          "measured_exchange_us": sim.slab_exchange_us(),
-                                         "choice": "auto: overlap iff the measured block exchange exceeds the edge "
-                                                   "bands' break-even (ws_autotune.cpp choose_slab_schedule)"
+                                         "choice": "auto: the first run of >= 2 blocks times one block of each "
+                                                   "schedule and keeps the faster (ws_schedule.cpp run_steps)"
                                                    if os.environ.get("WS_SLAB_OVERLAP") is None else
                                                    "fixed by WS_SLAB_OVERLAP"}}
                       if world > 1 else {})},

@@ -316,21 +316,15 @@ void autotune(ws_sim* s) {
     else autotune_t<float>(s);
 }
 
-// Overlap or stream-ordered slab blocks, decided from a MEASURED halo
-// exchange: the overlap schedule's edge bands cost extra stencil work (their warm-up rows) and
-// two cross-stream waits per block, which hiding the exchange repays only when the exchange
-// takes longer than that. Break-even exchange times per block, measured on one MI355X with
-// tools/rank_timing.py (C2 slabs of 2048 / 1024 / 512 rows, direct transport, block 6):
-// ~2 / ~20 / ~35 us; slabs thinner than three block depths have no interior to overlap.
-// Rank 0 times the block-depth exchange of the current state (RCCL, on the compute stream,
-// one warm-up + the mean of three: the halo rows are refreshed again at the run's start) and
-// broadcasts its decision, so every rank runs the same schedule.
-static double break_even_us(int rows) {
-    if (rows >= 2048) return 2.0;
-    if (rows >= 1024) return 20.0;
-    return 35.0;
-}
-
+// Overlap or stream-ordered slab blocks, decided by MEASURING both: the
+// overlap schedule's edge bands cost extra stencil work (their warm-up rows) and two cross-stream
+// waits per block, which hiding the exchange repays only when the exchange takes long enough --
+// and where that break-even lies depends on the slab's rows, the kernel and the link. Here rank 0
+// times the block-depth exchange of the current state (RCCL on the compute stream, one warm-up +
+// the mean of three; reported by ws_sim_slab_exchange_us), and where the slabs have an interior
+// to overlap (>= three block depths) the next run of >= two blocks times one block of each
+// schedule and keeps the faster (run_steps, ws_schedule.cpp: the slowest rank's times decide,
+// so every rank runs the same schedule).
 void choose_slab_schedule(ws_sim* s) {
     const int nst = fused_stages(s);
     const int depth = s->block * nst;
@@ -353,9 +347,13 @@ void choose_slab_schedule(ws_sim* s) {
         (void)hipEventDestroy(e1);
         us = ms * 1000.0 / 3.0;
     }
-    int32_t v[2] = {room && us > break_even_us(thin) ? 1 : 0, (int32_t)std::lround(us * 1000.0)};  // ns
+    int32_t v[2] = {room ? 1 : 0, (int32_t)std::lround(us * 1000.0)};  // ns
     if (s->comm && s->comm->nranks() > 1) s->comm->broadcast_i32(v, 2, 0, s->stream);
-    s->overlap = v[0] != 0;
+    s->overlap = false;  // stream-ordered until the trial decides
+    s->overlap_trial = v[0] != 0;
+    if (s->overlap_trial)
+        for (auto& e : s->ev_trial)
+            if (!e) WS_HIP_CHECK(hipEventCreate(&e));
     s->xfer_us = v[1] / 1000.0;
 }
 

@@ -564,26 +564,56 @@ void run_steps(ws_sim* s, int k) {
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
     }
-    const bool ovl = k > 0 && overlap_active(s);
-    if (ovl) ensure_overlap_grids(s);
-    for (int i = 0; i < k;) {
-        // overlap schedule: one block per iteration; else one launch
-        const int n = ovl ? std::min(s->block, k - i) : launch_steps(s, k - i);
-        if (ovl) {
-            if (s->dtype == WS_F64) overlap_block<double>(s, n, i == 0, i + n == k);
-            else overlap_block<float>(s, n, i == 0, i + n == k);
-        } else if (s->dtype == WS_F64) {
-            enqueue_steps<double>(s, n);
-        } else {
-            enqueue_steps<float>(s, n);
+    // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
+    // schedule's blocks (edge bands + exchange on the edge stream, interior on the compute stream)
+    auto segment = [&](int n_steps, bool ovl) {
+        if (n_steps <= 0) return;
+        if (ovl) ensure_overlap_grids(s);
+        s->block_pos = 0;
+        for (int i = 0; i < n_steps;) {
+            const int n = ovl ? std::min(s->block, n_steps - i) : launch_steps(s, n_steps - i);
+            if (ovl) {
+                if (s->dtype == WS_F64) overlap_block<double>(s, n, i == 0, i + n == n_steps);
+                else overlap_block<float>(s, n, i == 0, i + n == n_steps);
+            } else if (s->dtype == WS_F64) {
+                enqueue_steps<double>(s, n);
+            } else {
+                enqueue_steps<float>(s, n);
+            }
+            for (int j = 0; j < n; ++j) {
+                s->time = advance_time(s, s->time);
+                s->step++;
+            }
+            i += n;
         }
-        for (int j = 0; j < n; ++j) {
-            s->time = advance_time(s, s->time);
-            s->step++;
+        if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
+    };
+    if (k > 0 && s->overlap_trial && k >= 2 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): one block stream-ordered, one
+        // overlapped, each timed to completion (both give the same bits, so these are real
+        // steps of the run); the slower rank's time decides, identically on every rank
+        auto timed = [&](bool ovl) {
+            WS_HIP_CHECK(hipEventRecord(s->ev_trial[0], s->stream));
+            segment(s->block, ovl);
+            WS_HIP_CHECK(hipEventRecord(s->ev_trial[1], s->stream));
+            WS_HIP_CHECK(hipEventSynchronize(s->ev_trial[1]));
+            float ms = 0.f;
+            WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
+            return (double)ms;
+        };
+        double so = timed(false), ov = timed(true);
+        if (s->comm && s->comm->nranks() > 1) {
+            so = s->comm->allreduce_max(so, s->stream);
+            ov = s->comm->allreduce_max(ov, s->stream);
         }
-        i += n;
+        s->trial_ms[0] = so;
+        s->trial_ms[1] = ov;
+        s->overlap = ov < so;
+        s->overlap_trial = false;
+        segment(k - 2 * s->block, s->overlap && overlap_active(s));
+    } else {
+        segment(k, k > 0 && overlap_active(s));
     }
-    if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     if (s->aux_active) {
         WS_HIP_CHECK(hipEventRecord(s->aux_out, s->aux));
         WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->aux_out, 0));

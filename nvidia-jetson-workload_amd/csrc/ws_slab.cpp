@@ -151,6 +151,7 @@ int ws_sim_set_slab_schedule(ws_sim_t* s, int32_t block, int32_t overlap) {
         s->overlap_mode = overlap;
         s->overlap = overlap == WS_OVERLAP_ON;
         s->xfer_us = -1.0;  // auto: measured again at the next run
+        s->overlap_trial = false;
     });
 }
 
