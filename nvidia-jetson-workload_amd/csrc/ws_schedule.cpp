@@ -588,10 +588,12 @@ void run_steps(ws_sim* s, int k) {
         }
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 2 * s->block) {
-        // the auto schedule's decision (choose_slab_schedule): one block stream-ordered, one
-        // overlapped, each timed to completion (both give the same bits, so these are real
-        // steps of the run); the slower rank's time decides, identically on every rank
+    if (k > 0 && s->overlap_trial && k >= 4 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): one block of each schedule
+        // untimed (first launches of its shapes, the overlap grids, the chain tables), then one
+        // stream-ordered and one overlapped block, each timed to completion (both give the same
+        // bits, so these are real steps of the run); the slower rank's times decide, identically
+        // on every rank
         auto timed = [&](bool ovl) {
             WS_HIP_CHECK(hipEventRecord(s->ev_trial[0], s->stream));
             segment(s->block, ovl);
@@ -601,6 +603,8 @@ void run_steps(ws_sim* s, int k) {
             WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
             return (double)ms;
         };
+        segment(s->block, false);
+        segment(s->block, true);
         double so = timed(false), ov = timed(true);
         if (s->comm && s->comm->nranks() > 1) {
             so = s->comm->allreduce_max(so, s->stream);
@@ -610,7 +614,7 @@ void run_steps(ws_sim* s, int k) {
         s->trial_ms[1] = ov;
         s->overlap = ov < so;
         s->overlap_trial = false;
-        segment(k - 2 * s->block, s->overlap && overlap_active(s));
+        segment(k - 4 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
     }
