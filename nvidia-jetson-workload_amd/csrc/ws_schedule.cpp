@@ -566,7 +566,7 @@ void run_steps(ws_sim* s, int k) {
     }
     // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
     // schedule's blocks (edge bands + exchange on the edge stream, interior on the compute stream)
-    auto segment = [&](int n_steps, bool ovl) {
+    auto segment = [&](int n_steps, bool ovl, hipEvent_t after_first = nullptr) {
         if (n_steps <= 0) return;
         if (ovl) ensure_overlap_grids(s);
         s->block_pos = 0;
@@ -584,27 +584,26 @@ void run_steps(ws_sim* s, int k) {
                 s->time = advance_time(s, s->time);
                 s->step++;
             }
+            if (i == 0 && after_first) WS_HIP_CHECK(hipEventRecord(after_first, s->stream));
             i += n;
         }
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 4 * s->block) {
-        // the auto schedule's decision (choose_slab_schedule): one block of each schedule
-        // untimed (first launches of its shapes, the overlap grids, the chain tables), then one
-        // stream-ordered and one overlapped block, each timed to completion (both give the same
-        // bits, so these are real steps of the run); the slower rank's times decide, identically
-        // on every rank
+    if (k > 0 && s->overlap_trial && k >= 6 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): three blocks of each schedule,
+        // timed from the end of the first to the end of the third -- the steady state (a run's
+        // first overlapped block exchanges its halo before any interior work; first launches of
+        // new shapes, the overlap grids and chain tables are set up in the first block). Both
+        // give the same bits, so these are real steps of the run; the slower rank's times decide,
+        // identically on every rank.
         auto timed = [&](bool ovl) {
-            WS_HIP_CHECK(hipEventRecord(s->ev_trial[0], s->stream));
-            segment(s->block, ovl);
+            segment(3 * s->block, ovl, s->ev_trial[0]);
             WS_HIP_CHECK(hipEventRecord(s->ev_trial[1], s->stream));
             WS_HIP_CHECK(hipEventSynchronize(s->ev_trial[1]));
             float ms = 0.f;
             WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
-            return (double)ms;
+            return (double)ms / 2.0;  // per block
         };
-        segment(s->block, false);
-        segment(s->block, true);
         double so = timed(false), ov = timed(true);
         if (s->comm && s->comm->nranks() > 1) {
             so = s->comm->allreduce_max(so, s->stream);
@@ -614,7 +613,7 @@ void run_steps(ws_sim* s, int k) {
         s->trial_ms[1] = ov;
         s->overlap = ov < so;
         s->overlap_trial = false;
-        segment(k - 4 * s->block, s->overlap && overlap_active(s));
+        segment(k - 6 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
     }
