@@ -183,9 +183,7 @@ __global__ __launch_bounds__(kFusedCols, WS_FUSED_MINW) void fused_step_kernel(F
         using Q3c = std::integral_constant<int, 6 + cur>;
 
         Y[yi(kPf)] = load_row(R + kPf);  // its slot held row R + kPf - kU: dead
-#if WS_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);  // keep the loads at the head of the body
-#endif
         pub(Q0c{}, Y[yi(0)]);
 
         if constexpr (on(1)) {

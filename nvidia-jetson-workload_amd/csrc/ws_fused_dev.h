@@ -15,13 +15,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 
 using U2 = unsigned int __attribute__((ext_vector_type(2)));
 using U4 = unsigned int __attribute__((ext_vector_type(4)));
-#ifndef WS_SCHED_BARRIER
-#define WS_SCHED_BARRIER 1  // pin each row's loads at the head of the march body
-#endif
-#ifndef WS_STORE_NT
-#define WS_STORE_NT 1
-#endif
-constexpr int kNT = WS_STORE_NT ? 2 : 0;  // cache policy bit: nontemporal (streamed output)
+// cache policy bit of the output stores: nontemporal (streamed output; cached stores measured
+// -5 % at C3 and +3 % at C2)
+constexpr int kNT = 2;
 constexpr uint32_t kDropped = 0x80000000u;  // voffset past every descriptor's range: op dropped
 
 // V is any 4-, 8- or 16-byte value type (float, double, float2, double2)

@@ -38,6 +38,7 @@
 #include <utility>
 
 #include "ws_fused_dev.h"
+#include "ws_knobs.h"
 
 namespace ws {
 namespace {  // kernels: internal to each translation unit
@@ -132,12 +133,6 @@ __device__ __forceinline__ void lds_lr(const P2<T>* row, int lane, const P2<T>& 
 // step per launch, exact fp64): 2 or 3 groups measured -3 / -8 %; round 2 (two steps per
 // launch, fast fp64: bodies twice as long, so one group gave the DMA ~1000 cycles): 2 groups
 // +9 %, 3 groups +0 %.
-#ifndef WS_DPPY_PF
-#define WS_DPPY_PF 0
-#endif
-#ifndef WS_DPPY_LDSX
-#define WS_DPPY_LDSX -1
-#endif
 
 // Workgroup barrier ordering LDS traffic only (no global-memory fence: the DMA prefetch stays
 // in flight across it)
@@ -168,15 +163,10 @@ struct StepRings {
 // kLag = 2 march bodies behind the producer; an LDS-only workgroup barrier every 2 bodies hands
 // the rows over (the consumer reads rows the producer finished before the last barrier, the
 // producer overwrites slots the consumer finished before it: kU >= 6 ring slots).
-#ifndef WS_PC_LAG  // measurement builds: the consumer's lag = the barrier interval, in bodies
-#define WS_PC_LAG 2
-#endif
-constexpr int kLag = WS_PC_LAG;
+constexpr int kLag = 2;  // the consumer's lag = the barrier interval, in bodies (1 measured 1 % slower)
 
-#ifndef WS_PC_MINW  // the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), fp64 pairs 2
-#define WS_PC_MINW 0
-#endif
-constexpr int pc_min_waves(int cpl, int elem) { return WS_PC_MINW > 0 ? WS_PC_MINW : cpl == 2 && elem == 8 ? 2 : 4; }
+// the producer / consumer kernel: 4 waves per SIMD (128 VGPRs), fp64 pairs 2
+constexpr int pc_min_waves(int cpl, int elem) { return cpl == 2 && elem == 8 ? 2 : 4; }
 
 // Diagnostic builds only (tools/wave_timeline.py, -DWS_WAVE_STAMPS): each workgroup's first lane
 // records its start / end time (100 MHz real-time counter and shader clock), its hardware
@@ -188,13 +178,7 @@ constexpr int kStampMax = 1 << 16;
 __device__ unsigned long long g_wave_stamps[kStampMax * kStampWords];
 #endif
 template <typename T, int NST, int NSTEP, int MODE, int CPL, bool SPLIT = false>
-#ifndef WS_DPPY_MINW  // measurement builds: minimum waves per SIMD the register allocation must allow
-#define WS_DPPY_MINW 1
-#endif
-#ifndef WS_PC_PF  // the producer's LDS-DMA prefetch distance in groups (0: 2 rows)
-#define WS_PC_PF 0
-#endif
-__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL, (int)sizeof(T)) : WS_DPPY_MINW) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
+__global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL, (int)sizeof(T)) : 1) void fused_dppy_kernel(FusedArgs<T> a, Geom g, int nstrips, int nsegs) {
     static_assert(CPL == 1 || CPL == 2, "one column or a column pair per lane");
     static_assert(!SPLIT || NSTEP == 2, "producer / consumer: a two-step launch");
     using VT = std::conditional_t<CPL == 1, T, P2<T>>;     // a lane's cells of one row
@@ -203,8 +187,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // 0.1162 ms/step at 4 rows against 2; C3 fp32 pairs: 0.0260 -> 0.0222 at 4 rows
     // against 2, 0.0256 at 6). The producer's bodies are one step long: at least 2 rows ahead
     // (fp64 / fp32 pairs: one group; fp64 pairs: two).
-    constexpr int kPF = SPLIT ? (WS_PC_PF > 0 ? WS_PC_PF : (2 / kG > 1 ? 2 / kG : 1))
-                              : WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
+    constexpr int kPF = SPLIT ? (2 / kG > 1 ? 2 / kG : 1) : WS_DPPY_PF > 0 ? WS_DPPY_PF : (4 / kG > 1 ? 4 / kG : 1);
     constexpr int kD = kG * kPF;
     constexpr int kR = kG > 2 ? kG : 2;                     // ring granule: whole groups, even
     constexpr int kNR = (kD + kG + 2 + kR - 1) / kR * kR;   // ring: rows R-2 .. R+kD+kG-1
@@ -613,13 +596,6 @@ namespace {
 
 // Launch fused_dppy_kernel<T, nstages, NSTEP, mode, CPL> (one translation unit per (T,
 // NSTEP, CPL): ws_fused_dppy{,2}_<t>_<n>.hip, compiled in parallel).
-// measurement builds only (-DWS_DPPY_LDS_PAD=bytes): unused dynamic LDS per wave, capping the
-// waves per SIMD for occupancy A/B runs
-#ifdef WS_DPPY_LDS_PAD
-constexpr unsigned kLdsPad = WS_DPPY_LDS_PAD;
-#else
-constexpr unsigned kLdsPad = 0;
-#endif
 
 // Workgroups of fused_dppy_kernel<T, nstages, NSTEP, mode, CPL, SPLIT> one CU holds at once
 // (the chain schedule's round size is this times the CU count).
@@ -629,7 +605,7 @@ int dppy_blocks_per_cu_impl(int nstages, int sp_mode) {
     const int threads = SPLIT ? 2 * kWave : kWave;
 #define WS_DPPY_OCC(N, M)                                                                                            \
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>, \
-                                                       threads, kLdsPad)
+                                                       threads, 0)
 #define WS_DPPY_O1(M) WS_DPPY_OCC(1, M)
 #define WS_DPPY_O2(M) WS_DPPY_OCC(2, M)
 #define WS_DPPY_O4(M) WS_DPPY_OCC(4, M)
@@ -651,7 +627,7 @@ hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, h
     const dim3 grid((unsigned)(a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L)),
         block(SPLIT ? 2 * kWave : kWave);
 #define WS_DPPY_GO(N, M) \
-    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>), grid, block, kLdsPad, s, a, g, nstrips, nsegs)
+    hipLaunchKernelGGL((fused_dppy_kernel<T, N, NSTEP, M, CPL, SPLIT>), grid, block, 0, s, a, g, nstrips, nsegs)
 #define WS_DPPY_G1(M) WS_DPPY_GO(1, M)
 #define WS_DPPY_G2(M) WS_DPPY_GO(2, M)
 #define WS_DPPY_G4(M) WS_DPPY_GO(4, M)

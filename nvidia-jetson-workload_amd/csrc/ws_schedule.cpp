@@ -168,9 +168,6 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
                 tab.push_back(per[gi][c]);
                 t.max_rows = std::max(t.max_rows, per[gi][c].y1 - per[gi][c].y0);
             }
-#ifdef WS_CHAIN_REVERSE  // measurement builds: the table in reverse order (bottom rows on the first XCDs)
-    std::reverse(tab.begin(), tab.end());
-#endif
     t.n = (int32_t)tab.size();
     WS_HIP_CHECK(hipMalloc(&t.dev, tab.size() * sizeof(ws::ChainSeg)));
     WS_HIP_CHECK(hipMemcpy(t.dev, tab.data(), tab.size() * sizeof(ws::ChainSeg), hipMemcpyHostToDevice));

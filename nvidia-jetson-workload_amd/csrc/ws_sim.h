@@ -123,10 +123,8 @@ namespace wsr {
 
 // row pitch (elements) and level stride of a W x H grid: rows padded to 64 elements, kHalo
 // halo rows above and below every level (the layout ws_slab_exchange_plan reports)
-#ifndef WS_PITCH_PAD  // measurement builds only (tools/variant.sh): extra elements per row
-#define WS_PITCH_PAD 0
-#endif
-inline int64_t layout_pitch(int64_t W) { return (W + 63) / 64 * 64 + WS_PITCH_PAD; }
+// (row pitch padding by 8 / 64 / 128 elements measured +-1 %)
+inline int64_t layout_pitch(int64_t W) { return (W + 63) / 64 * 64; }
 inline int64_t layout_lstride(int64_t H, int64_t pitch) { return (H + 2 * ws::kHalo) * pitch; }
 
 void grid_free(ws_grid* g);

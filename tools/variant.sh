@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build an A/B measurement variant of libws_hip.so with extra -D flags on one kernel file
 # (default ws_fused_dppy_f64_2.hip = the fp64 two-step dppy / x2y instantiations; e.g.
-# ws_runtime.cpp with -DWS_PITCH_PAD=64 for a padded row pitch):
-#   tools/variant.sh NAME "-DWS_DPP_PF=5 ..." [file]  -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
+# the knobs in csrc/ws_knobs.h):
+#   tools/variant.sh NAME "-DWS_DPPY_PF=3 ..." [file]  -> nvidia-jetson-workload_amd/lib/variants/libws_hip_NAME.so
 set -eu
 cd "$(dirname "$0")/../nvidia-jetson-workload_amd/csrc"
 make -s -j8 >/dev/null
