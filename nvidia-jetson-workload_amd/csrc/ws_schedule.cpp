@@ -586,22 +586,25 @@ void run_steps(ws_sim* s, int k) {
         }
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 6 * s->block) {
-        // the auto schedule's decision (choose_slab_schedule): three blocks of each schedule,
-        // timed from the end of the first to the end of the third -- the steady state (a run's
-        // first overlapped block exchanges its halo before any interior work; first launches of
-        // new shapes, the overlap grids and chain tables are set up in the first block). Both
-        // give the same bits, so these are real steps of the run; the slower rank's times decide,
-        // identically on every rank.
+    if (k > 0 && s->overlap_trial && k >= 8 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): two-block segments alternating
+        // stream-ordered / overlapped / stream-ordered / overlapped, each timed over its second
+        // block -- the steady state (a run's first overlapped block exchanges its halo before any
+        // interior work; first launches of new shapes, the overlap grids and chain tables are set
+        // up in the first block) -- and the better of the two samples per schedule compared, so a
+        // clock still ramping up favours neither. Both give the same bits, so these are real steps
+        // of the run; the slower rank's times decide, identically on every rank.
         auto timed = [&](bool ovl) {
-            segment(3 * s->block, ovl, s->ev_trial[0]);
+            segment(2 * s->block, ovl, s->ev_trial[0]);
             WS_HIP_CHECK(hipEventRecord(s->ev_trial[1], s->stream));
             WS_HIP_CHECK(hipEventSynchronize(s->ev_trial[1]));
             float ms = 0.f;
             WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
-            return (double)ms / 2.0;  // per block
+            return (double)ms;
         };
         double so = timed(false), ov = timed(true);
+        so = std::min(so, timed(false));
+        ov = std::min(ov, timed(true));
         if (s->comm && s->comm->nranks() > 1) {
             so = s->comm->allreduce_max(so, s->stream);
             ov = s->comm->allreduce_max(ov, s->stream);
@@ -610,7 +613,7 @@ void run_steps(ws_sim* s, int k) {
         s->trial_ms[1] = ov;
         s->overlap = ov < so;
         s->overlap_trial = false;
-        segment(k - 6 * s->block, s->overlap && overlap_active(s));
+        segment(k - 8 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
     }

@@ -7,3 +7,5 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 150 --timeout-method threa
 rc=$?; echo "slab tests rc=$rc"; tail -3 gpurun_out/t_slab.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python tools/rank_timing.py --config c2 --ranks 2,4,8 --xfer-us 0,40,80 --variants off,on,auto > gpurun_out/rank_timing_c2.txt 2>&1
 echo "rank c2 rc=$?"; cat gpurun_out/rank_timing_c2.txt
+timeout -k 10 300 python tools/pin_timing.py --config c2 --pins auto,dppy:2:-2:0,dppy:2:56:0 > gpurun_out/pins_h_c2.log 2>&1
+echo "pins rc=$?"; cat gpurun_out/pins_h_c2.log
