@@ -563,7 +563,8 @@ void run_steps(ws_sim* s, int k) {
     }
     // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
     // schedule's blocks (edge bands + exchange on the edge stream, interior on the compute stream)
-    auto segment = [&](int n_steps, bool ovl, hipEvent_t after_first = nullptr) {
+    // (marks: events recorded on the compute stream after the first and the second block)
+    auto segment = [&](int n_steps, bool ovl, hipEvent_t mark0 = nullptr, hipEvent_t mark1 = nullptr) {
         if (n_steps <= 0) return;
         if (ovl) ensure_overlap_grids(s);
         s->block_pos = 0;
@@ -581,22 +582,24 @@ void run_steps(ws_sim* s, int k) {
                 s->time = advance_time(s, s->time);
                 s->step++;
             }
-            if (i == 0 && after_first) WS_HIP_CHECK(hipEventRecord(after_first, s->stream));
+            const int prev = i;
             i += n;
+            if (mark0 && prev < s->block && i >= s->block) WS_HIP_CHECK(hipEventRecord(mark0, s->stream));
+            if (mark1 && prev < 2 * s->block && i >= 2 * s->block) WS_HIP_CHECK(hipEventRecord(mark1, s->stream));
         }
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 8 * s->block) {
-        // the auto schedule's decision (choose_slab_schedule): two-block segments alternating
-        // stream-ordered / overlapped / stream-ordered / overlapped, each timed over its second
-        // block -- the steady state (a run's first overlapped block exchanges its halo before any
-        // interior work; first launches of new shapes, the overlap grids and chain tables are set
-        // up in the first block) -- and the better of the two samples per schedule compared, so a
-        // clock still ramping up favours neither. Both give the same bits, so these are real steps
-        // of the run; the slower rank's times decide, identically on every rank.
+    if (k > 0 && s->overlap_trial && k >= 12 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): three-block segments alternating
+        // stream-ordered / overlapped / stream-ordered / overlapped, each timed over its middle
+        // block -- the steady state: a run's first overlapped block exchanges its halo before any
+        // interior work (and first launches of new shapes, the overlap grids and chain tables are
+        // set up in the first block), its last block has no next halo to exchange -- and the
+        // better of the two samples per schedule compared, so a clock still ramping up favours
+        // neither. Both give the same bits, so these are real steps of the run; the slower rank's
+        // times decide, identically on every rank.
         auto timed = [&](bool ovl) {
-            segment(2 * s->block, ovl, s->ev_trial[0]);
-            WS_HIP_CHECK(hipEventRecord(s->ev_trial[1], s->stream));
+            segment(3 * s->block, ovl, s->ev_trial[0], s->ev_trial[1]);
             WS_HIP_CHECK(hipEventSynchronize(s->ev_trial[1]));
             float ms = 0.f;
             WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
@@ -613,7 +616,7 @@ void run_steps(ws_sim* s, int k) {
         s->trial_ms[1] = ov;
         s->overlap = ov < so;
         s->overlap_trial = false;
-        segment(k - 8 * s->block, s->overlap && overlap_active(s));
+        segment(k - 12 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
     }
