@@ -116,12 +116,16 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
                 total += gr.wx * r.rows();
                 groups.push_back(gr);
             }
-    // chains per group in proportion to its cost (largest remainder), at least one, at most one per row
+    // chains per group in proportion to its cost (largest remainder), at least one, and none
+    // shorter than the march's warm-up (2 x the cone): a thin band -- an overlapped block's edge
+    // bands, launched beside the interior -- gets few long chains, not a chip's worth of stubs
+    const int min_rows = 2 * cone;
+    auto cap = [&](const Group& gr) { return std::max(1, gr.r.rows() / min_rows); };
     int64_t assigned = 0;
     for (Group& gr : groups) {
         const double ideal = (double)want * gr.wx * gr.r.rows() / total;
         gr.n = (int)std::max(1.0, std::floor(ideal));
-        gr.n = std::min(gr.n, gr.r.rows());
+        gr.n = std::min(gr.n, cap(gr));
         gr.frac = ideal - std::floor(ideal);
         assigned += gr.n;
     }
@@ -130,7 +134,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return groups[x].frac > groups[y].frac; });
     for (size_t i = 0; assigned < want && i < order.size(); ++i) {
         Group& gr = groups[order[i]];
-        if (gr.n < gr.r.rows()) { ++gr.n; ++assigned; }
+        if (gr.n < cap(gr)) { ++gr.n; ++assigned; }
     }
     // rows of each group's chains: equal cost, the chains in a y edge's cone priced kYClampCost
     auto yclamped = [&](int y0, int y1) { return (g->top_clamp && y0 < cone) || (g->bot_clamp && y1 > g->H - cone); };
