@@ -642,7 +642,7 @@ def main():
                    **({"slab_schedule": {"steps_per_exchange": block,
                                          "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap],
                                          "measured_exchange_us": sim.slab_exchange_us(),
-                                         "choice": "auto: the first run of >= 12 blocks times the middle blocks of alternating "
+                                         "choice": "auto: the first run of >= 12 blocks times the last two blocks of alternating "
                                                    "three-block segments of each schedule, best of two, and keeps the faster (ws_schedule.cpp run_steps)"
                                                    if os.environ.get("WS_SLAB_OVERLAP") is None else
                                                    "fixed by WS_SLAB_OVERLAP"}}

@@ -323,7 +323,7 @@ void autotune(ws_sim* s) {
 // times the block-depth exchange of the current state (RCCL on the compute stream, one warm-up +
 // the mean of three; reported by ws_sim_slab_exchange_us), and where the slabs have an interior
 // to overlap (>= three block depths) the next run of >= twelve blocks times each schedule's steady
-// blocks (three-block segments, alternating, the middle block of each timed) and keeps the faster (run_steps, ws_schedule.cpp: the slowest rank's times decide,
+// blocks (three-block segments, alternating, the last two blocks of each timed) and keeps the faster (run_steps, ws_schedule.cpp: the slowest rank's times decide,
 // so every rank runs the same schedule).
 void choose_slab_schedule(ws_sim* s) {
     const int nst = fused_stages(s);

@@ -203,7 +203,7 @@ struct ws_sim {
     double xfer_us = -1.0;                // measured halo exchange (auto mode), microseconds
     bool overlap_trial = false;           // auto mode: time one block of each schedule at the next run
     double trial_ms[2] = {-1.0, -1.0};    // that trial: ms per block stream-ordered, overlapped
-    hipEvent_t ev_trial[3] = {};
+    hipEvent_t ev_trial[2] = {};
     hipStream_t edge = nullptr;
     hipEvent_t ev_edge = nullptr, ev_join = nullptr;
     ws_grid* ov[4] = {};      // interior ping-pong (0, 1), edge-band ping-pong (2, 3); u, v, h

@@ -165,7 +165,7 @@ def test_emulated_slab_measurement_aid(ovl, monkeypatch):
 def test_auto_schedule_from_measured_trial(xfer_us, expect, monkeypatch):
     """WS_OVERLAP_AUTO (the multi-GPU default): the first run times the block's halo exchange
     (reported); the first run of at least twelve blocks then alternates three-block segments of
-    each schedule, times their middle blocks and keeps the faster (ws_schedule.cpp run_steps). On the emulated slab the
+    each schedule, times their last two blocks and keeps the faster (ws_schedule.cpp run_steps). On the emulated slab the
     exchange is a timed wait of xfer_us: none -> the overlap's extra edge launches lose; 150 us
     -> hiding the wait behind the interior wins."""
     monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
