@@ -264,8 +264,12 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // (no exec-mask branch). launch_fused_step_dppy checks the byte ranges fit.
     const int64_t lofs = (int64_t)level * g.lstride;
     const int rbase = max(y0 - kNS, row_lo);
-    // past the last row the march fetches (SPLIT: kLag more bodies, see march)
-    const int rtop = min(row_hi, y1 + kNS + (SPLIT ? kLag : 0) + kU + kD + kG);
+    // past the last input row the output rows [y0, y1) depend on (their cone: y1 + kNS - 1).
+    // The march's prefetch runs further -- kD rows ahead, rounded up to its unroll, SPLIT's
+    // lag -- but rows past the cone feed only rows that are never stored, so their DMAs are
+    // left out of range: the buffer range check drops them without a memory access (round 4:
+    // up to kU + kD + kG + kLag rows of HBM reads per segment or chain saved)
+    const int rtop = min(row_hi, y1 + kNS);
     const uint32_t in_bytes = (uint32_t)((int64_t)(rtop - rbase) * g.pitch * sizeof(T));
     const uint32_t out_bytes = (uint32_t)((int64_t)(y1 - y0) * g.pitch * sizeof(T));
     const int64_t ib = lofs + (int64_t)rbase * g.pitch, ob = lofs + (int64_t)y0 * g.pitch;
