@@ -28,14 +28,19 @@ static void autotune_time(ws_sim* s) {
     const int fixed_seg = s->seg_override;
     const int fixed_tb = s->tb;
     const int fixed_kernel = s->kernel;
-    // two steps per launch only where a run can use them (slab blocks of >= 2 steps)
-    const bool tb2_ok = s->block >= 2 || s->nranks == 1;
+    // multi-step launches only where a run can use them (slab blocks of >= tb steps)
     for (int k : {kKernDppLdsY, kKernX2Y, kKernPc, kKernPc2, kKernLds})
-      for (int tb : {1, 2}) {
+      for (int tb : {1, 2, 4}) {
         if (s->kernel_fixed && k != fixed_kernel) continue;  // pinned kernel: tune the rest for it
-        if (tb == 2 && (k == kKernLds || !tb2_ok)) continue;
-        if (tb == 1 && ws::fused_split(k)) continue;  // a two-step split (its one-step launches are dppy's / x2y's)
-        if (s->tb_fixed && k != kKernLds && tb != fixed_tb) continue;
+        if (tb > 1 && s->nranks > 1 && s->block < tb) continue;
+        // (the split variants are two-step launches only: their one-step launches are dppy's /
+        // x2y's; four steps: Euler / RK2 on the one-wave march, ws::fused_tb_ok)
+        if (k == kKernLds ? tb != 1 : !ws::fused_tb_ok(k, tb, nst, (int)elem_size(s->dtype))) continue;
+        if (s->tb_fixed && k != kKernLds) {  // a pinned 4 means 2 where this kernel / integrator takes no 4
+            int t = fixed_tb;
+            while (t > 1 && !ws::fused_tb_ok(k, t, nst, (int)elem_size(s->dtype))) t /= 2;
+            if (tb != t) continue;
+        }
         s->tb = tb;
         const int cone = nst * tb;
         for (bool al : {false, true}) {
@@ -238,7 +243,8 @@ static void tune_file_load_locked() {
                                   &c.align, &c.tb, &used);
         if (n != 15 || line[used] != 0) continue;  // exactly 15 fields
         const bool kernel_ok = c.kernel == kKernLds || ws::fused_is_dppy(c.kernel);
-        const bool tb_ok = c.tb == 1 || (c.tb == 2 && ws::fused_is_dppy(c.kernel));
+        const bool tb_ok = c.kernel == kKernLds ? c.tb == 1
+                                                : ws::fused_tb_ok(c.kernel, c.tb, k.nst, (int)elem_size(k.dtype));
         const bool seg_ok = (c.seg > 0 && c.seg <= k.H) ||
                             (ws::fused_is_dppy(c.kernel) && chain_rounds(c.seg) > 0 && chain_rounds(c.seg) <= kMaxChainRounds);
         if (kernel_ok && tb_ok && seg_ok && (c.align == 0 || c.align == 1) && k.W > 0 && k.H > 0 && k.L > 0)

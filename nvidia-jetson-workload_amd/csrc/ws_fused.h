@@ -99,7 +99,8 @@ hipError_t launch_fused_step(int nstages, const FusedArgs<T>& a, const Geom& g, 
 // "dppy": independent 64-lane waves, one column per lane, horizontal neighbours by DPP lane
 // shifts, y rows staged by LDS-DMA and read from LDS in place. "x2y": the same kernel with an
 // adjacent column pair per lane (128-column strips). variant = kFusedDppLdsY or kFusedX2Y;
-// nsteps = time steps per launch (1, or 2: temporal blocking, see ws_fused_dppy_kernel.h)
+// nsteps = time steps per launch (1, 2 or 4: temporal blocking, see ws_fused_dppy_kernel.h;
+// fused_tb_ok says which)
 template <typename T>
 hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const FusedArgs<T>& a, const Geom& g,
                                   hipStream_t s);
@@ -133,6 +134,16 @@ inline bool fused_is_dppy(int variant) {
 }
 inline bool fused_pairs(int variant) { return variant == kFusedX2Y || variant == kFusedPc2; }
 inline bool fused_split(int variant) { return variant == kFusedPc || variant == kFusedPc2; }
+// steps per launch a variant can take: 1 and 2 (the split variants: 2 only); 4 for the
+// one-wave march at Euler / RK2 (an 8-deep cone, the RK4 two-step kernel's) in fp32, and fp64
+// one column per lane (fp64 pairs would need > 256 VGPRs)
+inline bool fused_tb_ok(int variant, int tb, int nstages, int elem_bytes) {
+    if (tb == 1) return !fused_split(variant);
+    if (tb == 2) return fused_is_dppy(variant);
+    if (tb == 4)
+        return (variant == kFusedDppLdsY || (variant == kFusedX2Y && elem_bytes == 4)) && nstages <= 2;
+    return false;
+}
 inline int fused_strip_cols(int variant) {
     return fused_pairs(variant) ? 128 : fused_is_dppy(variant) ? 64 : 256;
 }

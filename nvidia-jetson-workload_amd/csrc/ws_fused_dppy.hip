@@ -1,5 +1,6 @@
 // Host launcher of the dppy / x2y fused step kernel (kernel: ws_fused_dppy_kernel.h; its
-// instantiations: ws_fused_dppy{,2}_{f32,f64}_{1,2}.hip).
+// instantiations: ws_fused_dppy{,2}_{f32,f64}_{1,2}.hip, and the four-step launches
+// ws_fused_dppy_{f32,f64}_4.hip, ws_fused_dppy2_f32_4.hip).
 #include "ws_fused.h"
 
 namespace ws {
@@ -9,7 +10,8 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
                                   hipStream_t s) {
     const int out_w = a.out_w;
     if (!fused_is_dppy(variant)) return hipErrorInvalidValue;
-    if (nsteps != 1 && nsteps != 2) return hipErrorInvalidValue;
+    if (!fused_tb_ok(variant, nsteps, nstages, (int)sizeof(T)) && !(fused_split(variant) && nsteps == 1))
+        return hipErrorInvalidValue;
     const int ns = nstages * nsteps;  // the launch's cone depth
     if (out_w < 1 || out_w > fused_strip_cols(variant) - 2 * fused_margin(variant, ns, (int)sizeof(T)))
         return hipErrorInvalidValue;
@@ -30,9 +32,15 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     if (fused_split(variant) && nsteps == 2)
         return fused_pairs(variant) ? launch_dppy_pc_tu<T, 2>(nstages, a, g, s, nstrips, nsegs)
                                     : launch_dppy_pc_tu<T, 1>(nstages, a, g, s, nstrips, nsegs);
-    if (fused_pairs(variant))
+    if (fused_pairs(variant)) {
+        if (nsteps == 4) {
+            if constexpr (sizeof(T) == 4) return launch_dppy_tu<T, 4, 2>(nstages, a, g, s, nstrips, nsegs);
+            return hipErrorInvalidValue;
+        }
         return nsteps == 1 ? launch_dppy_tu<T, 1, 2>(nstages, a, g, s, nstrips, nsegs)
                            : launch_dppy_tu<T, 2, 2>(nstages, a, g, s, nstrips, nsegs);
+    }
+    if (nsteps == 4) return launch_dppy_tu<T, 4, 1>(nstages, a, g, s, nstrips, nsegs);
     return nsteps == 1 ? launch_dppy_tu<T, 1, 1>(nstages, a, g, s, nstrips, nsegs)
                        : launch_dppy_tu<T, 2, 1>(nstages, a, g, s, nstrips, nsegs);
 }
@@ -42,8 +50,14 @@ int fused_dppy_blocks_per_cu(int variant, int nstages, int nsteps, int sp_mode) 
     if (fused_split(variant) && nsteps == 2)
         return fused_pairs(variant) ? dppy_pc_blocks_per_cu_tu<T, 2>(nstages, sp_mode)
                                     : dppy_pc_blocks_per_cu_tu<T, 1>(nstages, sp_mode);
-    if (fused_pairs(variant))
+    if (fused_pairs(variant)) {
+        if (nsteps == 4) {
+            if constexpr (sizeof(T) == 4) return dppy_blocks_per_cu_tu<T, 4, 2>(nstages, sp_mode);
+            return 0;
+        }
         return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 2>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 2>(nstages, sp_mode);
+    }
+    if (nsteps == 4) return dppy_blocks_per_cu_tu<T, 4, 1>(nstages, sp_mode);
     return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 1>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 1>(nstages, sp_mode);
 }
 template int fused_dppy_blocks_per_cu<float>(int, int, int, int);

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     constexpr int kNW = (kWarm + kU - 1) / kU < 3 ? (kWarm + kU - 1) / kU : 3;
     // a group's DMA may overwrite only slots whose rows were read in an earlier body
     static_assert(kU % kG == 0 && kU % 2 == 0 && kU % kNR == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
-    static_assert(NSTEP == 1 || NSTEP == 2, "one or two steps per launch");
+    static_assert(NSTEP == 1 || NSTEP == 2 || (NSTEP == 4 && !SPLIT), "one, two or four steps per launch");
     // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory LOADS
     // issued after them (the DMAs in between, incl. the reading body's own). Stores are not
     // counted: a store may complete before an older load, so a count that includes them can
@@ -454,20 +454,22 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         // keep the row's DMA at the head of the body: the scheduler would otherwise sink it
         // below the stencil math, shortening the prefetch distance
         __builtin_amdgcn_sched_barrier(0);
-        V3<VT> o0 = Z;
-        step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o0);
-        if constexpr (NSTEP == 1) {
-            if constexpr (On{}(NST)) store_row(R - NST, o0);
-            else store_row(y0 - 1, Z);
-        } else {
-            // step 2's input rows R-NST (just computed), R-NST-1, R-NST-2 (step 1's ring)
-            const V3<VT> i1 = st[0].O[r2(-NST - 1)], i2 = st[0].O[r2(-NST - 2)];
-            if constexpr (On{}(NST)) st[0].O[r2(-NST)] = o0;  // the slot of row R-NST-2, read above
-            V3<VT> o1 = Z;
-            step(std::integral_constant<int, 1>{}, Pc, Xc, Yc, On{}, st[1], o0, i1, i2, R - NST, o1);
-            if constexpr (On{}(2 * NST)) store_row(R - 2 * NST, o1);
-            else store_row(y0 - 1, Z);
-        }
+        V3<VT> o = Z;
+        step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o);
+        // step q's input rows R-qNST (step q-1's output, just computed), R-qNST-1, R-qNST-2
+        // (step q-1's output ring)
+        [&]<int... Qs>(std::integer_sequence<int, Qs...>) {
+            ([&] {
+                constexpr int q = Qs + 1;
+                const V3<VT> i1 = st[q - 1].O[r2(-q * NST - 1)], i2 = st[q - 1].O[r2(-q * NST - 2)];
+                if constexpr (On{}(q * NST)) st[q - 1].O[r2(-q * NST)] = o;  // the slot of row R-qNST-2, read above
+                V3<VT> oq = Z;
+                step(std::integral_constant<int, q>{}, Pc, Xc, Yc, On{}, st[q], o, i1, i2, R - q * NST, oq);
+                o = oq;
+            }(), ...);
+        }(std::make_integer_sequence<int, NSTEP - 1>{});
+        if constexpr (On{}(NSTEP * NST)) store_row(R - NSTEP * NST, o);
+        else store_row(y0 - 1, Z);
     };
 
     // SPLIT: the producer's body -- the first step at march row R, its output row R - NST into
@@ -616,7 +618,9 @@ int dppy_blocks_per_cu_impl(int nstages, int sp_mode) {
     switch (nstages) {
         case 1: WS_SP_DISPATCH(sp_mode, WS_DPPY_O1) break;
         case 2: WS_SP_DISPATCH(sp_mode, WS_DPPY_O2) break;
-        case 4: WS_SP_DISPATCH(sp_mode, WS_DPPY_O4) break;
+        case 4:  // (four-step launches: Euler / RK2 only -- an RK4 cone of 16)
+            if constexpr (NSTEP < 4) { WS_SP_DISPATCH(sp_mode, WS_DPPY_O4) }
+            break;
         default: return 0;
     }
 #undef WS_DPPY_O1
@@ -638,7 +642,10 @@ hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, h
     switch (nstages) {
         case 1: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G1) break;
         case 2: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G2) break;
-        case 4: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G4) break;
+        case 4:
+            if constexpr (NSTEP < 4) { WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G4) }
+            else return hipErrorInvalidValue;
+            break;
         default: return hipErrorInvalidValue;
     }
 #undef WS_DPPY_G1

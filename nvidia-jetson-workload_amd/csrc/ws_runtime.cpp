@@ -105,6 +105,13 @@ static void convert(Dst* d, const Src* s, size_t n) {
 
 }  // namespace wsr
 
+int ws_sim::launch_tb() const {
+    if (kernel == wsr::kKernLds) return 1;
+    int t = tb;
+    while (t > 1 && !ws::fused_tb_ok(kernel, t, wsr::fused_stages(this), (int)wsr::elem_size(dtype))) t /= 2;
+    return std::max(t, 1);
+}
+
 int32_t ws_sim::seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const {
     const ws_grid* g = slot[0];
     const int64_t per_seg = strips(nst * launch_tb()) * g->L;
@@ -200,7 +207,9 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         }
         if (const char* e = env_str("WS_TB")) {
             s->tb = std::atoi(e);
-            require(s->tb == 1 || s->tb == 2, WS_ERR_INVALID, "WS_TB must be 1 or 2");
+            // (4: where the kernel takes four steps -- Euler / RK2 on dppy, x2y in fp32 --
+            // else two: ws_sim::launch_tb)
+            require(s->tb == 1 || s->tb == 2 || s->tb == 4, WS_ERR_INVALID, "WS_TB must be 1, 2 or 4");
             require(!(s->kernel_env && ws::fused_split(s->kernel) && s->tb == 1), WS_ERR_INVALID,
                     "WS_KERNEL=pc / pc2 advance two steps per launch: WS_TB must be 2 (or unset)");
             s->tb_fixed = true;
@@ -911,8 +920,8 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
         require(s != nullptr, WS_ERR_INVALID, "null sim");
         require(kernel == -1 || kernel == kKernLds || ws::fused_is_dppy(kernel), WS_ERR_INVALID,
                 "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y, WS_KERNEL_PC or WS_KERNEL_PC2");
-        require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2, WS_ERR_INVALID,
-                "steps_per_launch must be -1, 1 or 2");
+        require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2 || steps_per_launch == 4,
+                WS_ERR_INVALID, "steps_per_launch must be -1, 1, 2 or 4");
         require(seg_rows == -1 || seg_rows > 0 || (chain_rounds(seg_rows) > 0 && chain_rounds(seg_rows) <= kMaxChainRounds),
                 WS_ERR_INVALID, "seg_rows must be -1, positive, or -2 .. -9 (chain schedule of 1 .. 8 rounds)");
         require(align == -1 || align == 0 || align == 1, WS_ERR_INVALID, "align must be -1, 0 or 1");
@@ -921,7 +930,7 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
         require(!(k != -1 && ws::fused_split(k) && tb == 1), WS_ERR_INVALID,
                 "the split variants (WS_KERNEL_PC, WS_KERNEL_PC2) advance two steps per launch: "
                 "steps_per_launch must be 2 or -1");
-        require(!(k == kKernLds && tb == 2), WS_ERR_INVALID, "WS_KERNEL_LDS advances one step per launch");
+        require(!(k == kKernLds && tb > 1), WS_ERR_INVALID, "WS_KERNEL_LDS advances one step per launch");
         if (kernel != -1) { s->kernel = kernel; s->kernel_fixed = true; }
         if (steps_per_launch != -1) { s->tb = steps_per_launch; s->tb_fixed = true; }
         else if (k != -1 && ws::fused_split(k)) s->tb = 2;  // the only choice left for a split kernel

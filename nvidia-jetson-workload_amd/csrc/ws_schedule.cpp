@@ -358,13 +358,22 @@ bool config_spacing(const ws_sim* s) {
     return true;
 }
 
-// Steps the next launch advances, of `remaining`: 2 when the tuned configuration launches
-// two steps at once, the slab block has room for both, and both steps see the config's
-// spacing (the kernel's later stages use it); else 1.
+// The largest launch (4, 2 or 1 steps) of at most `room` steps the tuned configuration
+// allows: its steps per launch, and every step of a multi-step launch sees the config's
+// spacing (the kernel's later stages use it).
+static int launch_of(const ws_sim* s, int room) {
+    if (room < 2 || !use_fused(s) || s->launch_tb() < 2 || !config_spacing(s)) return 1;
+    for (int k : {4, 2})
+        if (k <= s->launch_tb() && k <= room &&
+            ws::fused_tb_ok(s->kernel, k, fused_stages(s), (int)elem_size(s->dtype)))
+            return k;
+    return 1;
+}
+
+// Steps the next launch advances, of `remaining` (a slab's block bounds it too: one domain
+// has no blocks).
 int launch_steps(const ws_sim* s, int remaining) {
-    if (remaining < 2 || !use_fused(s) || s->launch_tb() < 2) return 1;
-    if (s->nranks > 1 && s->block_pos + 2 > s->block) return 1;  // a slab's block (one domain: no blocks)
-    return config_spacing(s) ? 2 : 1;
+    return launch_of(s, s->nranks > 1 ? std::min(remaining, s->block - s->block_pos) : remaining);
 }
 
 // One time step on the stream (no host synchronisation).
@@ -397,10 +406,9 @@ static void enqueue_steps(ws_sim* s, int nsteps) {
 
 // steps per launch within a block (2 while the tuned configuration launches two at once)
 static std::vector<int> block_launches(const ws_sim* s, int steps) {
-    const bool two = use_fused(s) && s->launch_tb() >= 2 && config_spacing(s);
     std::vector<int> n;
     for (int left = steps; left > 0;) {
-        const int k = two && left >= 2 ? 2 : 1;
+        const int k = launch_of(s, left);
         n.push_back(k);
         left -= k;
     }

@@ -226,8 +226,9 @@ struct ws_sim {
     // cone = stages per launch (NST x steps per launch): the strip margins
     int out_w(int cone) const { return ws::fused_out_w(kernel, cone, (int)wsr::elem_size(dtype), align); }
     int64_t strips(int cone) const { return (slot[0]->W + out_w(cone) - 1) / out_w(cone); }
-    // steps per launch the tuned configuration asks for (1 unless dppy / x2y with tb = 2)
-    int launch_tb() const { return kernel == wsr::kKernLds ? 1 : tb; }
+    // steps per launch the tuned configuration launches where a run has room: tb, capped to
+    // what the kernel takes at this integrator and precision (ws::fused_tb_ok: 4 -> 2 -> 1)
+    int launch_tb() const;
     // segment rows giving about want_blocks workgroups (at least min_rows rows; the march
     // length rows + 2 NST a multiple of the unroll)
     int32_t seg_for_blocks(int nst, int64_t want_blocks, int64_t min_rows) const;

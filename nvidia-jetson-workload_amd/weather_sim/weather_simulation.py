@@ -702,8 +702,8 @@ class WeatherSimulation:
         return (out, ms.value) if with_time else out
 
     def steps_per_launch(self):
-        """Extension: time steps one fused launch advances inside run() (1, or 2 with temporal
-        blocking; ws_hip.h ws_sim_steps_per_launch)."""
+        """Extension: time steps one fused launch advances inside run() (1, or 2 / 4 with
+        temporal blocking; ws_hip.h ws_sim_steps_per_launch)."""
         n = ctypes.c_int32()
         check(lib.ws_sim_steps_per_launch(self._h, ctypes.byref(n)))
         return n.value

@@ -62,9 +62,9 @@ def test_default_numerics_by_precision(monkeypatch):
         s.set_numerics("approximate")
 
 
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"),
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("dppy", "4"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"),
                                       ("lds", "1")],
-                         ids=["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"])
+                         ids=["dppy", "dppy_tb2", "dppy_tb4", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"])
 def test_fast_matches_reference_fixtures(kernel, tb, monkeypatch):
     monkeypatch.setenv("WS_NUMERICS", "fast")
     monkeypatch.setenv("WS_KERNEL", kernel)
@@ -101,7 +101,7 @@ def test_fast_matches_reference_fixtures(kernel, tb, monkeypatch):
     print(f"{kernel}: worst relative L2 over {n_iso} fixture cases = {worst:.3e}")
 
 
-@pytest.mark.parametrize("tb", ["1", "2"])
+@pytest.mark.parametrize("tb", ["1", "2", "4"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 def test_fast_large_grid_vs_oracle(method, tb, monkeypatch):
     """4096 x 2048 fp64 (every strip / segment seam of the production tiling), 3 steps,
@@ -111,7 +111,7 @@ def test_fast_large_grid_vs_oracle(method, tb, monkeypatch):
     monkeypatch.setenv("WS_NUMERICS", "fast")
     monkeypatch.setenv("WS_KERNEL", "dppy")
     monkeypatch.setenv("WS_TB", tb)
-    W, H, steps = 4096, 2048, 3
+    W, H, steps = 4096, 2048, 5 if tb == "4" else 3  # (tb 4: a four-step launch where it applies)
     sim = make_sim(W, H, 0, method, True, f=1e-4)
     sim.set_initial_condition(ws.BreakingWaveInitialCondition(1.5, 0.05, 10.0))
     sim.initialize()

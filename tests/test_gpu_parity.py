@@ -58,12 +58,16 @@ def load(sim, s0):
 
 # (WS_FUSED, WS_KERNEL, WS_TB): every fused variant, dppy also with two steps per launch
 # (temporal blocking: run(n) advances pairs of steps per launch), and the per-stage kernels
-KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "x2y", "1"), ("1", "x2y", "2"), ("1", "pc", "2"), ("1", "pc2", "2"),
-           ("1", "lds", "1"), ("0", "x2y", "1")]
-KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_x2y", "fused_x2y_tb2", "fused_pc_tb2", "fused_pc2_tb2", "fused_lds", "stage_kernels"]
+# (tb 4: four steps per launch where the kernel takes them -- Euler / RK2 on dppy, x2y in
+# fp32 -- two elsewhere)
+KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "dppy", "4"), ("1", "x2y", "1"), ("1", "x2y", "2"),
+           ("1", "x2y", "4"), ("1", "pc", "2"), ("1", "pc2", "2"), ("1", "lds", "1"), ("0", "x2y", "1")]
+KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_dppy_tb4", "fused_x2y", "fused_x2y_tb2", "fused_x2y_tb4",
+              "fused_pc_tb2", "fused_pc2_tb2", "fused_lds", "stage_kernels"]
 # (kernel, steps per launch) of the fused variants
-FUSED = [("dppy", "1"), ("dppy", "2"), ("x2y", "1"), ("x2y", "2"), ("pc", "2"), ("pc2", "2"), ("lds", "1")]
-FUSED_IDS = ["dppy", "dppy_tb2", "x2y", "x2y_tb2", "pc_tb2", "pc2_tb2", "lds"]
+FUSED = [("dppy", "1"), ("dppy", "2"), ("dppy", "4"), ("x2y", "1"), ("x2y", "2"), ("x2y", "4"), ("pc", "2"),
+         ("pc2", "2"), ("lds", "1")]
+FUSED_IDS = ["dppy", "dppy_tb2", "dppy_tb4", "x2y", "x2y_tb2", "x2y_tb4", "pc_tb2", "pc2_tb2", "lds"]
 
 
 @pytest.mark.parametrize("fused,kernel,tb", KERNELS, ids=KERNEL_IDS)
@@ -266,16 +270,17 @@ def _dam_break(W, H, width_cells, dtype):
     return np.broadcast_to(row, (H, W)).astype(dtype)
 
 
-@pytest.mark.parametrize("tb", ["1", "2", "pc", "pc2", "chain"])
+@pytest.mark.parametrize("tb", ["1", "2", "4", "x2y4", "pc", "pc2", "chain"])
 @pytest.mark.parametrize("name", ["C1_dam_break_256_i0_f32", "C1_dam_break_256_i2_f32", "C2_dam_break_4096_i2_f64",
                                   "C2_dam_break_4096_i0_f64", "C2_jet_stream_4096_i2_f64",
                                   "C3_zonal_flow_2048_baro_f32"])
 def test_full_size_digests(name, tb, monkeypatch):
-    """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, pc /
-    pc2 the producer / consumer split of them (one column / a column pair per lane)."""
-    if tb in ("2", "pc", "pc2", "chain"):
-        monkeypatch.setenv("WS_KERNEL", tb if tb in ("pc", "pc2") else "dppy")
-        monkeypatch.setenv("WS_TB", "2")
+    """Full-size reference digests; tb = 2 pins the two-step launches (dppy) at full size, 4 /
+    x2y4 the four-step launches of dppy / x2y (Euler / RK2 cases; two steps for RK4), pc / pc2
+    the producer / consumer split of the two-step march (one column / a column pair per lane)."""
+    if tb in ("2", "4", "x2y4", "pc", "pc2", "chain"):
+        monkeypatch.setenv("WS_KERNEL", tb if tb in ("pc", "pc2") else "x2y" if tb == "x2y4" else "dppy")
+        monkeypatch.setenv("WS_TB", "4" if tb in ("4", "x2y4") else "2")
     if tb == "chain":  # the chain schedule, one round of the chip's resident waves
         monkeypatch.setenv("WS_SEG_ROWS", "-2")
     d = large_digests()[name]
@@ -455,7 +460,8 @@ def test_fused_non_pow2_spacing_vs_oracle():
 
 @pytest.mark.parametrize("kernel,seg_rows,tb", [("dppy", "6", "1"), ("dppy", "0", "1"), ("dppy", "6", "2"),
                                                  ("dppy", "0", "2"), ("x2y", "6", "1"), ("x2y", "0", "1"),
-                                                 ("x2y", "6", "2"), ("pc", "6", "2"), ("pc", "0", "2"), ("pc2", "6", "2"),
+                                                 ("x2y", "6", "2"), ("dppy", "0", "4"), ("x2y", "6", "4"),
+                                                 ("pc", "6", "2"), ("pc", "0", "2"), ("pc2", "6", "2"),
                                                  ("lds", "6", "1"), ("lds", "0", "1")])
 @pytest.mark.parametrize("nslabs", [2, 3, 5])
 @pytest.mark.parametrize("method", [0, 1, 2])
@@ -513,3 +519,28 @@ def test_slab_group_levels_and_pe():
     one.run(5)
     for name in ("u", "v", "h", "t", "p", "q"):
         np.testing.assert_array_equal(group.gather(name), one.get_current_grid()._get(name), err_msg=name)
+
+
+@pytest.mark.parametrize("kernel,fp64,method,want", [("x2y", False, 1, 4), ("dppy", False, 0, 4), ("dppy", True, 1, 4),
+                                                     ("x2y", True, 1, 2), ("dppy", False, 2, 2), ("pc", False, 1, 2)])
+def test_four_step_launches(kernel, fp64, method, want, monkeypatch):
+    """WS_TB=4: four steps per launch where the kernel takes them (Euler / RK2 on dppy, x2y in
+    fp32), two elsewhere; run(n) splits n into 4-, 2- and 1-step launches, and the result is
+    bit-for-bit the one-step run (ws_schedule.cpp launch_of)."""
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", str(want if want == 4 else 4))
+    sim = make_sim(300, 83, 0, method, fp64)
+    sim.set_initial_condition(ws.JetStreamInitialCondition())
+    sim.initialize()
+    assert sim.run(11) == 11
+    assert sim.steps_per_launch() == want
+    _, launches = sim.last_run_stats()
+    assert launches == (11 // 4 + 1 + 1 if want == 4 else 11 // 2 + 1)  # 4+4+2+1 / 2 x 5 + 1
+    monkeypatch.setenv("WS_TB", "1")
+    ref = make_sim(300, 83, 0, method, fp64)
+    ref.set_initial_condition(ws.JetStreamInitialCondition())
+    ref.initialize()
+    ref.run(11)
+    got, exp = state(sim.get_current_grid()), state(ref.get_current_grid())
+    for k in ("u", "v", "h", "vort"):
+        np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
