@@ -536,6 +536,7 @@ def test_four_step_launches(kernel, fp64, method, want, monkeypatch):
     assert sim.steps_per_launch() == want
     _, launches = sim.last_run_stats()
     assert launches == (11 // 4 + 1 + 1 if want == 4 else 11 // 2 + 1)  # 4+4+2+1 / 2 x 5 + 1
+    monkeypatch.setenv("WS_KERNEL", "dppy")
     monkeypatch.setenv("WS_TB", "1")
     ref = make_sim(300, 83, 0, method, fp64)
     ref.set_initial_condition(ws.JetStreamInitialCondition())
