@@ -152,7 +152,7 @@ struct StepRings {
     V3<VT> Y[2];                  // Y[r % 2] = the step's input row r, r <= R-3
     V3<VT> S1[2], S2[2], S3[2];   // [r % 2] = stage output at row r
     V3<VT> K2[2], K3[2];          // RK4 stage-2 tendency / stage-3 keep (rk4_keep3) at row r
-    V3<VT> O[4];                  // [r % 4] = the step's output row r (the next step's input), NSTEP > 1
+    V3<VT> O[2];                  // the step's last output rows (the next step's input), NSTEP > 1
 };
 
 // SPLIT (two steps per launch, one column per lane; variant "pc"): a workgroup of two waves on
@@ -203,15 +203,11 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // warm-up periods: stage gs (1..kNS) is needed from march row R - R0 >= 2 gs on (the
     // consumer's bodies lag kLag rows). At most three are peeled: a stage computed before it
     // enters the cone only reaches rows that are never stored (skipping it saves work only).
-    // one-wave march: step q runs kSL bodies behind step q-1 (ws_knobs.h WS_DPPY_SL)
-    constexpr int kSL = SPLIT ? 0 : WS_DPPY_SL;
-    constexpr int kSLT = kSL * (NSTEP - 1);  // the last step's total lag
-    constexpr int kWarm = 2 * kNS + (SPLIT ? kLag : 0) + kSLT;
+    constexpr int kWarm = 2 * kNS + (SPLIT ? kLag : 0);
     constexpr int kNW = (kWarm + kU - 1) / kU < 3 ? (kWarm + kU - 1) / kU : 3;
     // a group's DMA may overwrite only slots whose rows were read in an earlier body
     static_assert(kU % kG == 0 && kU % 2 == 0 && kU % kNR == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
     static_assert(NSTEP == 1 || NSTEP == 2 || (NSTEP == 4 && !SPLIT), "one, two or four steps per launch");
-    static_assert(NSTEP == 1 || SPLIT || kU % 4 == 0, "the output ring O[r % 4]: whole periods");
     // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory LOADS
     // issued after them (the DMAs in between, incl. the reading body's own). Stores are not
     // counted: a store may complete before an older load, so a count that includes them can
@@ -356,14 +352,11 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
 #pragma unroll
     for (int q = 0; q < NSTEP; ++q)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i < 2) st[q].Y[i] = st[q].S1[i] = st[q].S2[i] = st[q].S3[i] = st[q].K2[i] = st[q].K3[i] = Z;
-            st[q].O[i] = Z;
-        }
+        for (int i = 0; i < 2; ++i) st[q].Y[i] = st[q].S1[i] = st[q].S2[i] = st[q].S3[i] = st[q].K2[i] = st[q].K3[i] = st[q].O[i] = Z;
 
     const int R0 = y0 - kNS;
     // rounded up to the unroll (SPLIT: the consumer's bodies lag kLag rows behind the march)
-    const int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) + kSLT - R0 + kU - 1) / kU * kU;
+    const int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
 
     // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
     // stage s computes row Rq - s; the step's output row Rq - NST goes to `out`. Stage s of
@@ -448,10 +441,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     auto body = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
         constexpr int P = decltype(Pc)::value;
         constexpr int KW = decltype(KWc)::value;
-        struct On {  // (stage gs of step q = (gs - 1) / NST lags q kSL rows)
-            constexpr bool operator()(int gs) const { return KW < 0 || KW * kU + P >= 2 * gs + kSL * ((gs - 1) / NST); }
+        struct On {
+            constexpr bool operator()(int gs) const { return KW < 0 || KW * kU + P >= 2 * gs; }
         };
-        constexpr auto r4 = [](int d) { return ((P + d) % 4 + 4) % 4; };
+        constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         constexpr auto sl = [](int d) { return ((P + d) % kNR + kNR) % kNR; };  // ring slot of row R+d
         if constexpr (P % kG == 0) {
             dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies
@@ -463,29 +456,19 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         __builtin_amdgcn_sched_barrier(0);
         V3<VT> o = Z;
         step(std::integral_constant<int, 0>{}, Pc, Xc, Yc, On{}, st[0], yR0, yR1, yR2, R, o);
-        // step q marches at row R - q (NST + kSL): its input rows are step q-1's output rows
-        // R - q (NST + kSL) .. - 2. With kSL = 0 the first of them is the row step q-1 computed in
-        // this body (o); with kSL = 1 all three come from step q-1's output ring and this body's
-        // row goes into the ring after them (the slot of row - 3), so the two steps' stage chains
-        // are independent within a body.
+        // step q's input rows R-qNST (step q-1's output, just computed), R-qNST-1, R-qNST-2
+        // (step q-1's output ring)
         [&]<int... Qs>(std::integer_sequence<int, Qs...>) {
             ([&] {
                 constexpr int q = Qs + 1;
-                constexpr int d = -q * (NST + kSL);  // step q's march row, relative to R
+                const V3<VT> i1 = st[q - 1].O[r2(-q * NST - 1)], i2 = st[q - 1].O[r2(-q * NST - 2)];
+                if constexpr (On{}(q * NST)) st[q - 1].O[r2(-q * NST)] = o;  // the slot of row R-qNST-2, read above
                 V3<VT> oq = Z;
-                if constexpr (kSL == 0) {
-                    const V3<VT> i1 = st[q - 1].O[r4(d - 1)], i2 = st[q - 1].O[r4(d - 2)];
-                    if constexpr (On{}(q * NST)) st[q - 1].O[r4(d)] = o;
-                    step(std::integral_constant<int, q>{}, Pc, Xc, Yc, On{}, st[q], o, i1, i2, R + d, oq);
-                } else {
-                    const V3<VT> i0 = st[q - 1].O[r4(d)], i1 = st[q - 1].O[r4(d - 1)], i2 = st[q - 1].O[r4(d - 2)];
-                    if constexpr (On{}(q * NST)) st[q - 1].O[r4(d + kSL)] = o;  // row R+d+1: the slot of row R+d-3
-                    step(std::integral_constant<int, q>{}, Pc, Xc, Yc, On{}, st[q], i0, i1, i2, R + d, oq);
-                }
+                step(std::integral_constant<int, q>{}, Pc, Xc, Yc, On{}, st[q], o, i1, i2, R - q * NST, oq);
                 o = oq;
             }(), ...);
         }(std::make_integer_sequence<int, NSTEP - 1>{});
-        if constexpr (On{}(NSTEP * NST)) store_row(R - NSTEP * NST - kSLT, o);
+        if constexpr (On{}(NSTEP * NST)) store_row(R - NSTEP * NST, o);
         else store_row(y0 - 1, Z);
     };
 

@@ -14,11 +14,4 @@
 #ifndef WS_DPPY_LDSX
 #define WS_DPPY_LDSX -1
 #endif
-// march bodies step q of a multi-step launch runs behind step q-1 in the one-wave march (0:
-// step q reads the row step q-1 wrote in the same body -- one dependency chain through every
-// stage; 1: the two steps' stage chains are independent within a body, for one more row of
-// the output ring)
-#ifndef WS_DPPY_SL
-#define WS_DPPY_SL 0
-#endif
 // WS_WAVE_STAMPS: per-workgroup start / end / placement records (tools/wave_timeline.py)
