@@ -348,10 +348,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     };
 
     const V3<VT> Z{VT{}, VT{}, VT{}};
-    // WS_DPPY_DEFER: the row the previous body computed, stored after this body's DMA wait
-    constexpr bool kDefer = !SPLIT && WS_DPPY_DEFER != 0;
-    V3<VT> pend = Z;
-    int pend_j = y0 - 1;
     StepRings<VT> st[NSTEP];
 #pragma unroll
     for (int q = 0; q < NSTEP; ++q)
@@ -454,7 +450,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
             dma(R + kD, sl(kD));  // slots of rows R+kD-kNR.. (<= R-4): read in earlier bodies
             __builtin_amdgcn_s_waitcnt(waitcnt_vm(kWaitN));  // rows R .. R+kG-1 have landed
         }
-        if constexpr (kDefer) store_row(pend_j, pend);  // the previous body's row (WS_DPPY_DEFER)
         const V3<VT> yR0 = read_row(sl(0)), yR1 = read_row(sl(-1)), yR2 = read_row(sl(-2));
         // keep the row's DMA at the head of the body: the scheduler would otherwise sink it
         // below the stencil math, shortening the prefetch distance
@@ -473,14 +468,8 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                 o = oq;
             }(), ...);
         }(std::make_integer_sequence<int, NSTEP - 1>{});
-        if constexpr (kDefer) {
-            pend = On{}(NSTEP * NST) ? o : Z;
-            pend_j = On{}(NSTEP * NST) ? R - NSTEP * NST : y0 - 1;
-        } else if constexpr (On{}(NSTEP * NST)) {
-            store_row(R - NSTEP * NST, o);
-        } else {
-            store_row(y0 - 1, Z);
-        }
+        if constexpr (On{}(NSTEP * NST)) store_row(R - NSTEP * NST, o);
+        else store_row(y0 - 1, Z);
     };
 
     // SPLIT: the producer's body -- the first step at march row R, its output row R - NST into
@@ -562,7 +551,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
             }(), ...);
         }(std::make_integer_sequence<int, kNW>{});
         for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
-        if constexpr (kDefer) store_row(pend_j, pend);  // the last body's row
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     auto march = [&](auto Xc, auto Yc) {

@@ -14,11 +14,4 @@
 #ifndef WS_DPPY_LDSX
 #define WS_DPPY_LDSX -1
 #endif
-// one-wave march: a body's output row is stored by the NEXT body, right after its DMA wait
-// (1), instead of at the end of its own body (0). gfx9 counts stores in vmcnt too, so a DMA
-// wait (vmcnt <= the loads issued after the group) also waits for every store issued before
-// it: stored at the end of a body, a row's store has no time to complete before the next wait
-#ifndef WS_DPPY_DEFER
-#define WS_DPPY_DEFER 0
-#endif
 // WS_WAVE_STAMPS: per-workgroup start / end / placement records (tools/wave_timeline.py)
