@@ -279,8 +279,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                wh = make_rsrc(a.out_h + ob, out_bytes);
     const uint32_t row_bytes = (uint32_t)g.pitch * sizeof(T);
     const uint32_t soff = xout ? (uint32_t)x * sizeof(T) : kDropped;
-    // output stores' cache policy (ws_knobs.h WS_F32_STORE_POL for the fp32 kernels)
-    constexpr int kStorePol = sizeof(T) == 4 ? WS_F32_STORE_POL : kNT;
 
     // Stores are issued for every row, unconditionally: rows outside [y0, y1) are dropped by
     // the range check through the voffset (a branch around them makes the compiler's vmcnt
@@ -289,9 +287,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         const bool row_ok = j >= y0 && j < y1;
         const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
         const uint32_t vo = row_ok ? soff : kDropped;
-        buf_store_nt<VT, kStorePol>(o.u, wu, vo, so);
-        buf_store_nt<VT, kStorePol>(o.v, wv, vo, so);
-        buf_store_nt<VT, kStorePol>(o.h, wh, vo, so);
+        buf_store_nt<VT>(o.u, wu, vo, so);
+        buf_store_nt<VT>(o.v, wv, vo, so);
+        buf_store_nt<VT>(o.h, wh, vo, so);
     };
 
     // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG

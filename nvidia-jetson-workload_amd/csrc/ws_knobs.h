@@ -14,9 +14,4 @@
 #ifndef WS_DPPY_LDSX
 #define WS_DPPY_LDSX -1
 #endif
-// cache policy bits of the fp32 one-wave march's output stores (2: nontemporal, as fp64; 0:
-// cached -- the next launch's input of a grid that fits the Infinity Cache)
-#ifndef WS_F32_STORE_POL
-#define WS_F32_STORE_POL 2
-#endif
 // WS_WAVE_STAMPS: per-workgroup start / end / placement records (tools/wave_timeline.py)
