@@ -60,10 +60,12 @@ hipError_t launch_diagnostics(const T* u, const T* v, T* vort, T* div, const Spa
 template <typename T>
 hipError_t launch_affine(T* out, const T* in, T c, T tend, const Geom& g, hipStream_t s);
 // both PE updates in one pass: oT = iT + cT, oP = iP + cP (cX = dt * tendency, rounded in T);
-// nrep > 1 applies nrep steps' updates in one pass, each rounded: oT = ((iT + cT) + cT) ...
+// nrep > 1 applies nrep steps' updates in one pass, each rounded: oT = ((iT + cT) + cT) ...;
+// oT2 / oP2 (optional) receive the values after jrep (< nrep) of them in the same pass. The
+// outputs may alias the inputs (element-wise: each element is read before it is written).
 template <typename T>
 hipError_t launch_affine2(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP, const Geom& g, hipStream_t s,
-                          int nrep = 1);
+                          int nrep = 1, T* oT2 = nullptr, T* oP2 = nullptr, int jrep = 0);
 
 // fill all rows [0,H) of all levels with value
 template <typename T>

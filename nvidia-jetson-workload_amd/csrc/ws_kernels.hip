@@ -116,20 +116,31 @@ __global__ __launch_bounds__(kBX* kBY) void affine_kernel(T* __restrict__ out, c
 // rounding). Each level's rows [0, H) are one contiguous run of H * pitch elements (pitch
 // columns padded to 64 elements): 16-byte vectors over it, padding columns included (never
 // read as cells).
+// (The outputs may alias the inputs: every element is loaded before it is stored.)
 template <typename T>
-__global__ __launch_bounds__(256) void affine2_kernel(T* __restrict__ oT, const T* __restrict__ iT, T cT,
-                                                      T* __restrict__ oP, const T* __restrict__ iP, T cP,
-                                                      int64_t vec_per_level, int64_t lstride, int nrep) {
+__global__ __launch_bounds__(256) void affine2_kernel(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP,
+                                                      int64_t vec_per_level, int64_t lstride, int nrep, T* oT2,
+                                                      T* oP2, int jrep) {
     using V = T __attribute__((ext_vector_type(16 / sizeof(T))));
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= vec_per_level) return;
     const int64_t off = (int64_t)blockIdx.y * lstride + i * (int64_t)(16 / sizeof(T));
     V t = *(const V*)(iT + off);
     V p = *(const V*)(iP + off);
-    // nrep steps' updates, each rounded (no contraction in this build): (x + c) + c ...
+    V tj = t, pj = p;
+    // nrep steps' updates, each rounded (no contraction in this build): (x + c) + c ...; the
+    // values after jrep of them go to the second outputs
     for (int r = 0; r < nrep; ++r) {
         t = t + cT;
         p = p + cP;
+        if (r + 1 == jrep) {
+            tj = t;
+            pj = p;
+        }
+    }
+    if (oT2) {
+        __builtin_nontemporal_store(tj, (V*)(oT2 + off));
+        __builtin_nontemporal_store(pj, (V*)(oP2 + off));
     }
     __builtin_nontemporal_store(t, (V*)(oT + off));
     __builtin_nontemporal_store(p, (V*)(oP + off));
@@ -176,13 +187,15 @@ hipError_t launch_affine(T* out, const T* in, T c, T tend, const Geom& g, hipStr
 
 template <typename T>
 hipError_t launch_affine2(T* oT, const T* iT, T cT, T* oP, const T* iP, T cP, const Geom& g, hipStream_t s,
-                          int nrep) {
+                          int nrep, T* oT2, T* oP2, int jrep) {
     const int64_t n = (int64_t)g.H * g.pitch;
     if (n % (16 / (int64_t)sizeof(T)) != 0 || g.L > 65535 || nrep < 1) return hipErrorInvalidValue;
+    if ((oT2 == nullptr) != (oP2 == nullptr) || jrep < 0 || jrep >= nrep) return hipErrorInvalidValue;
     const int64_t nv = n / (16 / (int64_t)sizeof(T));
     if (nv <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nv + 255) / 256), (unsigned)g.L);
-    hipLaunchKernelGGL((affine2_kernel<T>), grid, dim3(256), 0, s, oT, iT, cT, oP, iP, cP, nv, g.lstride, nrep);
+    hipLaunchKernelGGL((affine2_kernel<T>), grid, dim3(256), 0, s, oT, iT, cT, oP, iP, cP, nv, g.lstride, nrep, oT2,
+                       oP2, jrep);
     return hipGetLastError();
 }
 
@@ -197,7 +210,8 @@ hipError_t launch_fill(T* out, T value, const Geom& g, hipStream_t s) {
     template hipError_t launch_diagnostics<T>(const T*, const T*, T*, T*, const Spacing<T>&, const Geom&,       \
                                               hipStream_t);                                                     \
     template hipError_t launch_affine<T>(T*, const T*, T, T, const Geom&, hipStream_t);                         \
-    template hipError_t launch_affine2<T>(T*, const T*, T, T*, const T*, T, const Geom&, hipStream_t, int);     \
+    template hipError_t launch_affine2<T>(T*, const T*, T, T*, const T*, T, const Geom&, hipStream_t, int, T*, \
+                                          T*, int);                                                             \
     template hipError_t launch_fill<T>(T*, T, const Geom&, hipStream_t);
 WS_INSTANTIATE(float)
 WS_INSTANTIATE(double)

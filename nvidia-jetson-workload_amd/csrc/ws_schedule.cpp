@@ -299,7 +299,11 @@ static void rotate(ws_sim* s, int nsteps) {
     ws_grid* c = s->slot[s->cur];
     ws_grid* n = s->slot[1 - s->cur];
     const bool pe = s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS;
-    if (pe) {
+    if (pe && s->tp_lazy) {
+        // inside run(): the drift is applied once, at the run's end (tp_flush)
+        s->tp_steps += nsteps;
+        s->tp_last = nsteps;
+    } else if (pe) {
         // stale tendency: the tendency grid's T/P keep their reset values 288.15f / 1013.25f
         // (`dt_ * tendency` has the same operands in every cell: one rounding, done here);
         // all nsteps updates in one pass, each rounded as the reference rounds it
@@ -316,13 +320,35 @@ static void rotate(ws_sim* s, int nsteps) {
         // two steps: exchange the storage of the fields written into the next grid (u, v, h
         // and, for PE, T and P), so the current grid holds the new state
         for (int f : {WS_FIELD_U, WS_FIELD_V, WS_FIELD_H, WS_FIELD_T, WS_FIELD_P}) {
-            if (!pe && (f == WS_FIELD_T || f == WS_FIELD_P)) continue;
+            if ((!pe || s->tp_lazy) && (f == WS_FIELD_T || f == WS_FIELD_P)) continue;  // (lazy: not written yet)
             std::swap(c->alloc[f], n->alloc[f]);
             std::swap(c->f[f], n->f[f]);
         }
         n->diag_pending = true;
     }
     s->slot[s->cur]->diag_pending = true;  // step() ends with calculateDiagnostics (:149)
+}
+
+// The PE T / P drift of a run, deferred by rotate() while tp_lazy: every launch of the run
+// moved T / P from the current grid to the next (each step's `+ dt tendency` rounded in turn)
+// and left the new values in the grid that ends current, the previous ones in the other --
+// so after launches n_1 .. n_m (k steps) the current grid holds T0 + k updates and the other
+// T0 + (k - n_m), T0 = the run's starting T (tp_src, which never moved: lazy launches swap no
+// T / P storage). One pass computes both (launch_affine2's second output), on the aux stream.
+template <typename T>
+static void tp_flush(ws_sim* s) {
+    s->tp_lazy = false;
+    if (s->tp_steps <= 0) return;
+    ws_grid* c = s->slot[s->cur];
+    ws_grid* n = s->slot[1 - s->cur];
+    const T dt = (T)s->dt;
+    const T cT = dt * T(288.15f), cP = dt * T(1013.25f);
+    WS_HIP_CHECK(ws::launch_affine2<T>((T*)c->f[WS_FIELD_T], (const T*)s->tp_src[0], cT, (T*)c->f[WS_FIELD_P],
+                                       (const T*)s->tp_src[1], cP, c->geom(), s->aux_active ? s->aux : s->stream,
+                                       (int)s->tp_steps, (T*)n->f[WS_FIELD_T], (T*)n->f[WS_FIELD_P],
+                                       (int)(s->tp_steps - s->tp_last)));
+    s->last_launches += 1;
+    s->tp_steps = 0;
 }
 
 // The halo exchange of a slab: RCCL (ws_comm.cpp), or -- the communicator-less measurement
@@ -572,6 +598,11 @@ void run_steps(ws_sim* s, int k) {
         }
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
+        // the T / P drift of the whole run in one pass at its end (tp_flush)
+        s->tp_lazy = true;
+        s->tp_steps = 0;
+        s->tp_src[0] = s->slot[s->cur]->f[WS_FIELD_T];
+        s->tp_src[1] = s->slot[s->cur]->f[WS_FIELD_P];
     }
     // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
     // schedule's blocks (edge bands + exchange on the edge stream, interior on the compute stream)
@@ -634,6 +665,10 @@ void run_steps(ws_sim* s, int k) {
         segment(k - 12 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
+    }
+    if (s->tp_lazy) {
+        if (s->dtype == WS_F64) tp_flush<double>(s);
+        else tp_flush<float>(s);
     }
     if (s->aux_active) {
         WS_HIP_CHECK(hipEventRecord(s->aux_out, s->aux));

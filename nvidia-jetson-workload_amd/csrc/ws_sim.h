@@ -173,6 +173,12 @@ struct ws_sim {
     hipStream_t aux = nullptr;
     hipEvent_t aux_in = nullptr, aux_out = nullptr;
     bool aux_active = false;
+    // PE T / P drift deferred inside run() (ws_schedule.cpp rotate / run_steps): the steps not
+    // yet applied, the last launch's steps, and the buffers holding the run's starting T / P
+    bool tp_lazy = false;
+    int64_t tp_steps = 0;
+    int tp_last = 0;
+    void* tp_src[2] = {nullptr, nullptr};
     double last_ms = 0.0;
     int64_t last_launches = 0;
     ws::KernelTimer timer;
