@@ -22,6 +22,10 @@ def test_scanner_flags_the_hazard():
     ok = ["buffer_store_dwordx4 v[0:3], v194, s[56:59], 0 offen nt", "s_nop 0", "v_add_u32_e32 v0, s8, v229"]
     other = ["buffer_store_dwordx4 v[0:3], v194, s[56:59], s10 offen nt", "v_add_u32_e32 v4, s8, v229"]
     assert len(scan(bad)) == 1 and not scan(ok) and not scan(other)
+    # global stores: vaddr first, vdata second (rewriting the address is no data hazard)
+    gbad = ["global_store_dwordx4 v[0:1], v[12:15], off nt", "v_mov_b32_e32 v13, 0"]
+    gaddr = ["global_store_dwordx4 v[0:1], v[12:15], off nt", "v_lshl_add_u64 v[0:1], s[14:15], 0, v[16:17]"]
+    assert len(scan(gbad)) == 1 and not scan(gaddr)
 
 
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump absent")

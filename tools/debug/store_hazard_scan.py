@@ -29,7 +29,9 @@ def scan(lines):
     for k, (n, t) in enumerate(ins[:-1]):
         if not _STORE.match(t):
             continue
-        data = _regs(t.split()[1].rstrip(","))
+        # the data operand: buffer_store vdata, vaddr, ...; global_store vaddr, vdata, saddr
+        ops = [o.rstrip(",") for o in t.split()[1:]]
+        data = _regs(ops[1] if t.startswith("global_") and len(ops) > 1 else ops[0])
         nxt = ins[k + 1][1]
         if nxt.startswith("v_") and len(nxt.split()) > 1 and _regs(nxt.split()[1].rstrip(",")) & data:
             hits.append((n, t, nxt))
