@@ -573,8 +573,8 @@ def main():
     # load, and W short warm-up steps from idle leave the timed steps on the ramp (measured:
     # C2 0.243 ms per two-step launch warm vs 0.277 when the timed run starts cold). Keep the
     # GPU busy for >= RAMP_S seconds of untimed steps first; reported as ramp_steps.
-    # (chunks of >= 12 blocks: the slab auto schedule's first such run holds its trial)
-    chunk = max(72, 12 * sim.slab_schedule()[0])
+    # (chunks of >= 16 blocks: the slab auto schedule's first such run holds its trial)
+    chunk = max(96, 16 * sim.slab_schedule()[0])
     ramp_steps = clock_ramp(lambda: sim.run(chunk), dist if world > 1 else None, args.warmup > 0)
     sim.set_kernel_timing(True, reserve=4 * args.steps + 16)  # events created outside the timed region
     barrier()
@@ -642,8 +642,8 @@ def main():
                    **({"slab_schedule": {"steps_per_exchange": block,
                                          "overlap": ["stream-ordered", "edge bands + exchange on a second stream"][overlap],
                                          "measured_exchange_us": sim.slab_exchange_us(),
-                                         "choice": "auto: the first run of >= 12 blocks times the last two blocks of alternating "
-                                                   "three-block segments of each schedule, best of two, and keeps the faster (ws_schedule.cpp run_steps)"
+                                         "choice": "auto: the first run of >= 16 blocks times the last three blocks of alternating "
+                                                   "four-block segments of each schedule, best of two, and keeps the faster (ws_schedule.cpp run_steps)"
                                                    if os.environ.get("WS_SLAB_OVERLAP") is None else
                                                    "fixed by WS_SLAB_OVERLAP"}}
                       if world > 1 else {})},

@@ -328,8 +328,8 @@ void autotune(ws_sim* s) {
 // and where that break-even lies depends on the slab's rows, the kernel and the link. Here rank 0
 // times the block-depth exchange of the current state (RCCL on the compute stream, one warm-up +
 // the mean of three; reported by ws_sim_slab_exchange_us), and where the slabs have an interior
-// to overlap (>= three block depths) the next run of >= twelve blocks times each schedule's steady
-// blocks (three-block segments, alternating, the last two blocks of each timed) and keeps the faster (run_steps, ws_schedule.cpp: the slowest rank's times decide,
+// to overlap (>= three block depths) the next run of >= sixteen blocks times each schedule's steady
+// blocks (four-block segments, alternating, the last three blocks of each timed) and keeps the faster (run_steps, ws_schedule.cpp: the slowest rank's times decide,
 // so every rank runs the same schedule).
 void choose_slab_schedule(ws_sim* s) {
     const int nst = fused_stages(s);

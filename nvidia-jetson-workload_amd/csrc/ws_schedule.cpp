@@ -632,24 +632,24 @@ void run_steps(ws_sim* s, int k) {
         if (mark1) WS_HIP_CHECK(hipEventRecord(mark1, s->stream));
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 12 * s->block) {
-        // the auto schedule's decision (choose_slab_schedule): three-block segments alternating
+    if (k > 0 && s->overlap_trial && k >= 16 * s->block) {
+        // the auto schedule's decision (choose_slab_schedule): four-block segments alternating
         // stream-ordered / overlapped / stream-ordered / overlapped, each timed on the compute
-        // stream from the end of its first block to the end of its last: two block periods in
+        // stream from the end of its first block to the end of its last: three block periods in
         // the steady state (a run's first overlapped block exchanges its halo before any interior
         // work, and first launches of new shapes, the overlap grids and chain tables are set up
-        // in it). Over two periods the overlap's whole dependency cycle is inside the window --
+        // in it). Over three periods the overlap's whole dependency cycle is inside the window --
         // interior k-1 -> edge bands k -> exchange -> interior k+1 -- so the exchange is charged
         // as far as the interior does not hide it. The better of the two samples per schedule is
         // compared, so a clock still ramping up favours neither. Both give the same bits, so
         // these are real steps of the run; the slower rank's times decide, identically on every
         // rank.
         auto timed = [&](bool ovl) {
-            segment(3 * s->block, ovl, s->ev_trial[0], s->ev_trial[1]);
+            segment(4 * s->block, ovl, s->ev_trial[0], s->ev_trial[1]);
             WS_HIP_CHECK(hipEventSynchronize(s->ev_trial[1]));
             float ms = 0.f;
             WS_HIP_CHECK(hipEventElapsedTime(&ms, s->ev_trial[0], s->ev_trial[1]));
-            return ms / 2.0;
+            return ms / 3.0;
         };
         double so = timed(false), ov = timed(true);
         so = std::min(so, timed(false));
@@ -662,7 +662,7 @@ void run_steps(ws_sim* s, int k) {
         s->trial_ms[1] = ov;
         s->overlap = ov < so;
         s->overlap_trial = false;
-        segment(k - 12 * s->block, s->overlap && overlap_active(s));
+        segment(k - 16 * s->block, s->overlap && overlap_active(s));
     } else {
         segment(k, k > 0 && overlap_active(s));
     }

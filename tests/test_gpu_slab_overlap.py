@@ -164,8 +164,8 @@ def test_emulated_slab_measurement_aid(ovl, monkeypatch):
 @pytest.mark.parametrize("xfer_us,expect", [(0.0, False), (150.0, True)])
 def test_auto_schedule_from_measured_trial(xfer_us, expect, monkeypatch):
     """WS_OVERLAP_AUTO (the multi-GPU default): the first run times the block's halo exchange
-    (reported); the first run of at least twelve blocks then alternates three-block segments of
-    each schedule, times their last two blocks and keeps the faster (ws_schedule.cpp run_steps). On the emulated slab the
+    (reported); the first run of at least sixteen blocks then alternates four-block segments of
+    each schedule, times their last three blocks and keeps the faster (ws_schedule.cpp run_steps). On the emulated slab the
     exchange is a timed wait of xfer_us: none -> the overlap's extra edge launches lose; 150 us
     -> hiding the wait behind the interior wins."""
     monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
@@ -173,11 +173,11 @@ def test_auto_schedule_from_measured_trial(xfer_us, expect, monkeypatch):
     assert sim.slab_exchange_us() == -1.0 and sim.slab_schedule() == (6, False)  # not measured yet
     sim.set_initial_condition(ws.JetStreamInitialCondition())
     sim.initialize()
-    assert sim.run(7) == 7  # fewer than twelve blocks: the exchange is timed, the trial waits
+    assert sim.run(7) == 7  # fewer than sixteen blocks: the exchange is timed, the trial waits
     us = sim.slab_exchange_us()
     assert us >= xfer_us * 0.9 and us < xfer_us + 1000.0
     assert sim.slab_schedule() == (6, False)
-    assert sim.run(80) == 80  # the trial (twelve blocks), then the faster schedule
+    assert sim.run(100) == 100  # the trial (sixteen blocks), then the faster schedule
     assert sim.slab_schedule() == (6, expect)
     assert np.isfinite(sim.get_current_grid()._get("h")).all()
     sim.set_slab_schedule(3, "off")  # fixed by the caller from now on
