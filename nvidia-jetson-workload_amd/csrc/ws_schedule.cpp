@@ -598,7 +598,12 @@ void run_steps(ws_sim* s, int k) {
         }
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
-        // the T / P drift of the whole run in one pass at its end (tp_flush)
+        // the T / P drift of the whole run in one pass at its end (tp_flush); a run that threw
+        // before its flush leaves its completed launches' drift to apply first
+        if (s->tp_lazy) {
+            if (s->dtype == WS_F64) tp_flush<double>(s);
+            else tp_flush<float>(s);
+        }
         s->tp_lazy = true;
         s->tp_steps = 0;
         s->tp_src[0] = s->slot[s->cur]->f[WS_FIELD_T];
