@@ -545,3 +545,25 @@ def test_four_step_launches(kernel, fp64, method, want, monkeypatch):
     got, exp = state(sim.get_current_grid()), state(ref.get_current_grid())
     for k in ("u", "v", "h", "vort"):
         np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+
+
+@pytest.mark.parametrize("tb", ["1", "2", "4"])
+@pytest.mark.parametrize("k", [1, 3, 7, 12])
+def test_pe_drift_once_per_run(k, tb, monkeypatch):
+    """PE T / P: run(k) applies the k steps' drift in one pass at its end (ws_schedule.cpp
+    tp_flush); the current grid's T and P equal k single step() calls bit for bit, with one-,
+    two- and four-step launches (fp32, RK2: the four-step kernel)."""
+    monkeypatch.setenv("WS_KERNEL", "x2y")
+    monkeypatch.setenv("WS_TB", tb)
+    sims = []
+    for _ in range(2):
+        sim = make_sim(200, 72, 2, 1, False, levels=3)
+        sim.set_initial_condition(ws.JetStreamInitialCondition())
+        sim.initialize()
+        sims.append(sim)
+    assert sims[0].run(k) == k
+    for _ in range(k):
+        sims[1].step()
+    a, b = sims[0].get_current_grid(), sims[1].get_current_grid()
+    for get in ("get_temperature_field", "get_pressure_field", "get_height_field"):
+        np.testing.assert_array_equal(getattr(a, get)(), getattr(b, get)(), err_msg=get)
