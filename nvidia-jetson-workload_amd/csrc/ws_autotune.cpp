@@ -67,8 +67,8 @@ static void autotune_time(ws_sim* s) {
                     segs.push_back(s->seg_for_blocks(nst, waves / wave_per_block, 5 * nst));
                 if (ws::fused_is_dppy(k)) {  // more waves per SIMD fit: shorter segments pay
                     for (int64_t waves : {8192, 12288}) segs.push_back(s->seg_for_blocks(nst, waves, 5 * nst));
-                    // the chain schedule: 1 / 2 / 3 rounds of the chip's resident workgroups
-                    for (int r : {1, 2, 3}) segs.push_back(seg_chains(r));
+                    // the chain schedule: 1, 2, 3, 4 or 6 chains (waves) per SIMD
+                    for (int r : {1, 2, 3, 4, 6}) segs.push_back(seg_chains(r));
                 }
                 std::sort(segs.begin(), segs.end());
                 segs.erase(std::unique(segs.begin(), segs.end()), segs.end());

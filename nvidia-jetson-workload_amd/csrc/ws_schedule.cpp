@@ -72,8 +72,7 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
     return {g->top_clamp ? 0 : -e, g->bot_clamp ? g->H : g->H + e};
 }
 
-// Chain schedule (ws_fused.h FusedArgs::chains): `rounds` x the workgroups the chip holds at
-// once, each marching ONE chain -- a run of rows of one strip (and level) -- sized so that every
+// Chain schedule (ws_fused.h FusedArgs::chains): `rounds` waves per SIMD, each marching ONE chain -- a run of rows of one strip (and level) -- sized so that every
 // chain of a launch costs about the same. A strip whose window touches a global x edge runs the
 // clamped march (kXClampCost x the instructions per row of an interior strip, the fp64 RK4
 // two-step kernel's steady loops: tools/isa_mix.py) and a chain reaching into a global y edge's
@@ -94,8 +93,11 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
         WS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
         s->num_cus = cus;
     }
-    const int bpc = ws::fused_dppy_blocks_per_cu<T>(s->kernel, nst, nsteps, sp_mode);
-    const int64_t want = (int64_t)rounds * std::max(1, bpc) * std::max(1, s->num_cus);
+    // `rounds` chains per SIMD (4 per CU; a split variant's workgroup is two waves): a whole
+    // number of waves on every SIMD whatever the kernel's occupancy (C3's launch with 1.5 waves
+    // per SIMD ran half its SIMDs idle for the last 40 %, profiles/r04_timeline_c3.txt)
+    const int waves_per_wg = ws::fused_split(s->kernel) ? 2 : 1;
+    const int64_t want = (int64_t)rounds * 4 * std::max(1, s->num_cus) / waves_per_wg;
     const int cone = nst * nsteps;
     const int nstrips = (g->W + out_w - 1) / out_w;
     struct Group {

@@ -246,7 +246,7 @@ struct ws_sim {
 
 namespace wsr {
 // A segment choice (seg_override, ws_sim_pin_variant's seg_rows) of -2, -3, ... selects the chain
-// schedule (ws_fused.h FusedArgs::chains) with 1, 2, ... rounds of the chip's resident workgroups.
+// schedule (ws_fused.h FusedArgs::chains) with 1, 2, ... chains (waves) per SIMD.
 inline int chain_rounds(int seg) { return seg <= -2 ? -seg - 1 : 0; }
 constexpr int seg_chains(int rounds) { return -(rounds + 1); }
 constexpr int kMaxChainRounds = 8;
