@@ -344,7 +344,7 @@ int ws_sim_kernel_timing(const ws_sim_t* sim, int32_t kind, int64_t* launches, d
  * 5 = the same with an adjacent column pair per lane (128 columns per wave), 6 = the DPP
  * kernel's two-step launch split over a producer wave (the first step) and a consumer wave
  * (the second) per strip, handing rows over through LDS (its one-step launches are kernel
- * 4's), 7 = the same split of kernel 5 (column pairs), -1 = per-stage kernels (ids 1-3 are retired variants); seg_rows = output rows per segment, out_cols =
+ * 4's), 7 = the same split of kernel 5 (column pairs), -1 = per-stage kernels (ids 1-3 are retired variants); seg_rows = output rows per segment (or -r - 1: r chains per SIMD), out_cols =
  * output columns per strip (a multiple of the 128-byte line when the strips are
  * line-aligned). Chosen by timing every variant on the real grid at the first run (all give
  * identical results), unless WS_KERNEL / WS_SEG_ROWS / ws_sim_pin_variant fix it. The
@@ -360,7 +360,8 @@ int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows
  * _PC2 advance two steps per launch: 1 is rejected, -1 means 2; _LDS one: 2 and 4 are rejected;
  * 4 = four steps where the kernel takes them -- Euler / RK2 with _DPPY, or _X2Y in fp32 -- else
  * two, as WS_TB=4);
- * seg_rows: output rows per segment; align: 1 = strip output windows on whole 128-byte lines.
+ * seg_rows: output rows per segment, or -2 .. -9 = the chain schedule with 1 .. 8 cost-balanced
+ * chains (one wave each) per SIMD; align: 1 = strip output windows on whole 128-byte lines.
  * The WS_KERNEL / WS_TB / WS_SEG_ROWS environment pins are process-wide and switch tuning off
  * (what they leave free takes its default; WS_KERNEL=pc|pc2 implies WS_TB=2). */
 #define WS_KERNEL_LDS 0
