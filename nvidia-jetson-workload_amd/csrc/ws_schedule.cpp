@@ -123,11 +123,17 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     // bands, launched beside the interior -- gets few long chains, not a chip's worth of stubs
     const int min_rows = 2 * cone;
     auto cap = [&](const Group& gr) { return std::max(1, gr.r.rows() / min_rows); };
+    // ... and none longer than a 32-bit buffer descriptor spans (the launcher's check: rows +
+    // 2 cone + 48 rows of pitch below 2^31 bytes; C5's 16384-row strips at one chain per strip)
+    const int64_t row_bytes = (int64_t)g->pitch * (int64_t)elem_size(s->dtype);
+    // (nine tenths of it: the y-edge weights below lengthen the other chains of a group a little)
+    const int max_rows = (int)std::max<int64_t>(min_rows, (0x7fffffff / row_bytes - 2 * cone - 64) * 9 / 10);
+    auto floor_n = [&](const Group& gr) { return (gr.r.rows() + max_rows - 1) / max_rows; };
     int64_t assigned = 0;
     for (Group& gr : groups) {
         const double ideal = (double)want * gr.wx * gr.r.rows() / total;
         gr.n = (int)std::max(1.0, std::floor(ideal));
-        gr.n = std::min(gr.n, cap(gr));
+        gr.n = std::max(floor_n(gr), std::min(gr.n, cap(gr)));
         gr.frac = ideal - std::floor(ideal);
         assigned += gr.n;
     }
