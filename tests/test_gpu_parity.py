@@ -281,7 +281,7 @@ def test_full_size_digests(name, tb, monkeypatch):
     if tb in ("2", "4", "x2y4", "pc", "pc2", "chain"):
         monkeypatch.setenv("WS_KERNEL", tb if tb in ("pc", "pc2") else "x2y" if tb == "x2y4" else "dppy")
         monkeypatch.setenv("WS_TB", "4" if tb in ("4", "x2y4") else "2")
-    if tb == "chain":  # the chain schedule, one round of the chip's resident waves
+    if tb == "chain":  # the chain schedule, one chain per SIMD
         monkeypatch.setenv("WS_SEG_ROWS", "-2")
     d = large_digests()[name]
     spec = {k: v for k, v in (l.split()[1:3] for l in d["spec"] if l.startswith("cfg "))}
@@ -318,7 +318,7 @@ def test_long_horizon_benched_workload(kernel, monkeypatch):
     exact numerics bitwise, and the default fast numerics (what the bench times) within the
     north_star tolerance of 1e-10 relative L2 per field of that exact (= reference) state.
     kernel None = the autotuned choice; else a pinned two-step variant (-chain: on the chain
-    schedule, one round of the chip's resident waves)."""
+    schedule, one chain per SIMD)."""
     if kernel:
         monkeypatch.setenv("WS_KERNEL", kernel.replace("-chain", ""))
         monkeypatch.setenv("WS_TB", "2")
