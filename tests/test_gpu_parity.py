@@ -377,7 +377,7 @@ def test_pe_levels_match_reference_per_level(kernel, tb, monkeypatch):
 def test_fused_tiling_vs_oracle(fp64, method, seg_rows, kernel, tb, monkeypatch):
     """Strip (x) and segment (y) seams of the fused kernel: 700 x 77 grid spans three
     256-lane strips and (with WS_SEG_ROWS) many ragged segments; bitwise vs the oracle.
-    seg_rows -2 / -4: the chain schedule (1 / 3 rounds of resident workgroups, chains of
+    seg_rows -2 / -4: the chain schedule (1 / 3 chains per SIMD, chains of
     cost-balanced lengths, y-clamped chains shorter)."""
     from oracle.ws_oracle import OracleSim
 
