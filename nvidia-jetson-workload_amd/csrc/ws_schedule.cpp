@@ -156,15 +156,6 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
         std::vector<double> w(n, 1.0);
         if (top) w[0] = kYClampCost;
         if (bot) w[n - 1] = n == 1 ? std::max(w[n - 1], kYClampCost) : kYClampCost;
-#if defined(WS_XCD_W6) || defined(WS_XCD_W7)
-        // measurement build: chains at the relative positions the table gives XCDs 6 / 7
-        // (xcd_work_item: contiguous eighths) priced dearer per row
-        for (int c = 0; c < n; ++c) {
-            const int x = std::min(7, c * 8 / std::max(1, n));
-            if (x == 6) w[c] *= WS_XCD_W6;
-            if (x == 7) w[c] *= WS_XCD_W7;
-        }
-#endif
         double inv = 0;
         for (double x : w) inv += 1.0 / x;
         int y = gr.r.y0;
