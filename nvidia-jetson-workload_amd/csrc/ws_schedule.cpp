@@ -645,7 +645,9 @@ void run_steps(ws_sim* s, int k) {
         if (mark1) WS_HIP_CHECK(hipEventRecord(mark1, s->stream));
         if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
-    if (k > 0 && s->overlap_trial && k >= 16 * s->block) {
+    // (the trial runs where the overlap schedule could: a fused slab with the configured spacing)
+    const bool trial_ok = (s->nranks > 1 || s->comm) && use_fused(s) && config_spacing(s);
+    if (k > 0 && s->overlap_trial && trial_ok && k >= 16 * s->block) {
         // the auto schedule's decision (choose_slab_schedule): four-block segments alternating
         // stream-ordered / overlapped / stream-ordered / overlapped, each timed on the compute
         // stream from the end of its first block to the end of its last: three block periods in
