@@ -28,7 +28,7 @@
  *   WS_NUMERICS=exact|fast    numerics of the fused kernels at creation (ws_sim_set_numerics)
  *   WS_FUSED=0                per-stage kernels instead of the fused step kernel
  *   WS_KERNEL=dppy|x2y|pc|pc2|lds (pin the fused-kernel variant)     } each also settable per
- *   WS_TB=1|2|4               pin the steps per fused launch    } simulation with
+ *   WS_TB=1|2|4|8             pin the steps per fused launch    } simulation with
  *   WS_SEG_ROWS=n             pin the rows per kernel segment   } ws_sim_pin_variant
  *   WS_AUTOTUNE=0|1|2         variant autotuner off / on (default) / on + print its table
  *   WS_TUNE_CACHE=path        append / reuse autotune choices across processes
@@ -356,10 +356,10 @@ int ws_sim_fused_variant(const ws_sim_t* sim, int32_t* kernel, int32_t* seg_rows
 /* Pin (part of) the fused-kernel variant of one simulation; -1 leaves a part to the
  * autotuner, which then times only candidates that agree with the pinned parts (a pinned
  * kernel gets its own best steps per launch, segment length and alignment). kernel:
- * WS_KERNEL_LDS / _DPPY / _X2Y / _PC / _PC2; steps_per_launch: 1, 2 or 4 (the split variants _PC /
+ * WS_KERNEL_LDS / _DPPY / _X2Y / _PC / _PC2; steps_per_launch: 1, 2, 4 or 8 (the split variants _PC /
  * _PC2 advance two steps per launch: 1 is rejected, -1 means 2; _LDS one: 2 and 4 are rejected;
  * 4 = four steps where the kernel takes them -- Euler / RK2 with _DPPY, or _X2Y in fp32 -- else
- * two, as WS_TB=4);
+ * two, as WS_TB=4; 8 = eight for Euler on the same kernels, else the largest they take);
  * seg_rows: output rows per segment, or -2 .. -9 = the chain schedule with 1 .. 8 cost-balanced
  * chains (one wave each) per SIMD; align: 1 = strip output windows on whole 128-byte lines.
  * The WS_KERNEL / WS_TB / WS_SEG_ROWS environment pins are process-wide and switch tuning off
@@ -373,8 +373,8 @@ int ws_sim_pin_variant(ws_sim_t* sim, int32_t kernel, int32_t steps_per_launch, 
 
 /* Time steps per fused launch the simulation's run() uses where it can (new; temporal
  * blocking): 1, 2 = the dppy-family kernel advances two steps per launch (y_n read once,
- * y_{n+2} written once), or 4 (Euler / RK2: four steps, y_n in and y_{n+4} out). Chosen by the
- * autotuner (WS_TB=1|2|4 fixes it). A k-step launch runs only inside run() with >= k steps
+ * y_{n+2} written once), 4 (Euler / RK2: four steps, y_n in and y_{n+4} out) or 8 (Euler).
+ * Chosen by the autotuner (WS_TB=1|2|4|8 fixes it). A k-step launch runs only inside run() with >= k steps
  * left, inside a slab block with room for them (else 2, then 1), and with the configured
  * spacing on both grids; results are identical to one-step launches. */
 int ws_sim_steps_per_launch(const ws_sim_t* sim, int32_t* steps);

@@ -30,11 +30,11 @@ static void autotune_time(ws_sim* s) {
     const int fixed_kernel = s->kernel;
     // multi-step launches only where a run can use them (slab blocks of >= tb steps)
     for (int k : {kKernDppLdsY, kKernX2Y, kKernPc, kKernPc2, kKernLds})
-      for (int tb : {1, 2, 4}) {
+      for (int tb : {1, 2, 4, 8}) {
         if (s->kernel_fixed && k != fixed_kernel) continue;  // pinned kernel: tune the rest for it
         if (tb > 1 && s->nranks > 1 && s->block < tb) continue;
         // (the split variants are two-step launches only: their one-step launches are dppy's /
-        // x2y's; four steps: Euler / RK2 on the one-wave march, ws::fused_tb_ok)
+        // x2y's; four steps: Euler / RK2 on the one-wave march, eight: Euler; ws::fused_tb_ok)
         if (k == kKernLds ? tb != 1 : !ws::fused_tb_ok(k, tb, nst, (int)elem_size(s->dtype))) continue;
         if (s->tb_fixed && k != kKernLds) {  // a pinned 4 means 2 where this kernel / integrator takes no 4
             int t = fixed_tb;

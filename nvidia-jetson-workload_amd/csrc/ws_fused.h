@@ -135,13 +135,15 @@ inline bool fused_is_dppy(int variant) {
 inline bool fused_pairs(int variant) { return variant == kFusedX2Y || variant == kFusedPc2; }
 inline bool fused_split(int variant) { return variant == kFusedPc || variant == kFusedPc2; }
 // steps per launch a variant can take: 1 and 2 (the split variants: 2 only); 4 for the
-// one-wave march at Euler / RK2 (an 8-deep cone, the RK4 two-step kernel's) in fp32, and fp64
-// one column per lane (fp64 pairs would need > 256 VGPRs)
+// one-wave march at Euler / RK2 and 8 at Euler (an 8-deep cone, the RK4 two-step kernel's) in
+// fp32, and fp64 one column per lane (fp64 pairs would need > 256 VGPRs)
 inline bool fused_tb_ok(int variant, int tb, int nstages, int elem_bytes) {
     if (tb == 1) return !fused_split(variant);
     if (tb == 2) return fused_is_dppy(variant);
     if (tb == 4)
         return (variant == kFusedDppLdsY || (variant == kFusedX2Y && elem_bytes == 4)) && nstages <= 2;
+    if (tb == 8)  // Euler: the same cone of 8
+        return (variant == kFusedDppLdsY || (variant == kFusedX2Y && elem_bytes == 4)) && nstages == 1;
     return false;
 }
 inline int fused_strip_cols(int variant) {

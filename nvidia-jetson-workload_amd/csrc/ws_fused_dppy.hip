@@ -1,6 +1,7 @@
 // Host launcher of the dppy / x2y fused step kernel (kernel: ws_fused_dppy_kernel.h; its
 // instantiations: ws_fused_dppy{,2}_{f32,f64}_{1,2}.hip, and the four-step launches
-// ws_fused_dppy_{f32,f64}_4.hip, ws_fused_dppy2_f32_4.hip).
+// ws_fused_dppy_{f32,f64}_4.hip, ws_fused_dppy2_f32_4.hip; eight-step (Euler) launches
+// ws_fused_dppy_{f32,f64}_8.hip, ws_fused_dppy2_f32_8.hip).
 #include "ws_fused.h"
 
 namespace ws {
@@ -33,14 +34,17 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
         return fused_pairs(variant) ? launch_dppy_pc_tu<T, 2>(nstages, a, g, s, nstrips, nsegs)
                                     : launch_dppy_pc_tu<T, 1>(nstages, a, g, s, nstrips, nsegs);
     if (fused_pairs(variant)) {
-        if (nsteps == 4) {
-            if constexpr (sizeof(T) == 4) return launch_dppy_tu<T, 4, 2>(nstages, a, g, s, nstrips, nsegs);
+        if (nsteps == 4 || nsteps == 8) {
+            if constexpr (sizeof(T) == 4)
+                return nsteps == 4 ? launch_dppy_tu<T, 4, 2>(nstages, a, g, s, nstrips, nsegs)
+                                   : launch_dppy_tu<T, 8, 2>(nstages, a, g, s, nstrips, nsegs);
             return hipErrorInvalidValue;
         }
         return nsteps == 1 ? launch_dppy_tu<T, 1, 2>(nstages, a, g, s, nstrips, nsegs)
                            : launch_dppy_tu<T, 2, 2>(nstages, a, g, s, nstrips, nsegs);
     }
     if (nsteps == 4) return launch_dppy_tu<T, 4, 1>(nstages, a, g, s, nstrips, nsegs);
+    if (nsteps == 8) return launch_dppy_tu<T, 8, 1>(nstages, a, g, s, nstrips, nsegs);
     return nsteps == 1 ? launch_dppy_tu<T, 1, 1>(nstages, a, g, s, nstrips, nsegs)
                        : launch_dppy_tu<T, 2, 1>(nstages, a, g, s, nstrips, nsegs);
 }
@@ -51,13 +55,16 @@ int fused_dppy_blocks_per_cu(int variant, int nstages, int nsteps, int sp_mode) 
         return fused_pairs(variant) ? dppy_pc_blocks_per_cu_tu<T, 2>(nstages, sp_mode)
                                     : dppy_pc_blocks_per_cu_tu<T, 1>(nstages, sp_mode);
     if (fused_pairs(variant)) {
-        if (nsteps == 4) {
-            if constexpr (sizeof(T) == 4) return dppy_blocks_per_cu_tu<T, 4, 2>(nstages, sp_mode);
+        if (nsteps == 4 || nsteps == 8) {
+            if constexpr (sizeof(T) == 4)
+                return nsteps == 4 ? dppy_blocks_per_cu_tu<T, 4, 2>(nstages, sp_mode)
+                                   : dppy_blocks_per_cu_tu<T, 8, 2>(nstages, sp_mode);
             return 0;
         }
         return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 2>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 2>(nstages, sp_mode);
     }
     if (nsteps == 4) return dppy_blocks_per_cu_tu<T, 4, 1>(nstages, sp_mode);
+    if (nsteps == 8) return dppy_blocks_per_cu_tu<T, 8, 1>(nstages, sp_mode);
     return nsteps == 1 ? dppy_blocks_per_cu_tu<T, 1, 1>(nstages, sp_mode) : dppy_blocks_per_cu_tu<T, 2, 1>(nstages, sp_mode);
 }
 template int fused_dppy_blocks_per_cu<float>(int, int, int, int);

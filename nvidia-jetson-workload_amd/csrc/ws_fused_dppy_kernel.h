@@ -207,7 +207,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     constexpr int kNW = (kWarm + kU - 1) / kU < 3 ? (kWarm + kU - 1) / kU : 3;
     // a group's DMA may overwrite only slots whose rows were read in an earlier body
     static_assert(kU % kG == 0 && kU % 2 == 0 && kU % kNR == 0 && kNR >= kD + kG + 2 && kD % kG == 0, "DMA ring");
-    static_assert(NSTEP == 1 || NSTEP == 2 || (NSTEP == 4 && !SPLIT), "one, two or four steps per launch");
+    static_assert(NSTEP == 1 || NSTEP == 2 || ((NSTEP == 4 || NSTEP == 8) && !SPLIT), "1, 2, 4 or 8 steps per launch");
     // Wait for a group's DMAs before reading it: vmcnt <= the number of vector-memory LOADS
     // issued after them (the DMAs in between, incl. the reading body's own). Stores are not
     // counted: a store may complete before an older load, so a count that includes them can
@@ -617,7 +617,9 @@ int dppy_blocks_per_cu_impl(int nstages, int sp_mode) {
 #define WS_DPPY_O4(M) WS_DPPY_OCC(4, M)
     switch (nstages) {
         case 1: WS_SP_DISPATCH(sp_mode, WS_DPPY_O1) break;
-        case 2: WS_SP_DISPATCH(sp_mode, WS_DPPY_O2) break;
+        case 2:  // (eight-step launches: Euler only)
+            if constexpr (NSTEP < 8) { WS_SP_DISPATCH(sp_mode, WS_DPPY_O2) }
+            break;
         case 4:  // (four-step launches: Euler / RK2 only -- an RK4 cone of 16)
             if constexpr (NSTEP < 4) { WS_SP_DISPATCH(sp_mode, WS_DPPY_O4) }
             break;
@@ -641,7 +643,10 @@ hipError_t launch_dppy_impl(int nstages, const FusedArgs<T>& a, const Geom& g, h
 #define WS_DPPY_G4(M) WS_DPPY_GO(4, M)
     switch (nstages) {
         case 1: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G1) break;
-        case 2: WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G2) break;
+        case 2:
+            if constexpr (NSTEP < 8) { WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G2) }
+            else return hipErrorInvalidValue;
+            break;
         case 4:
             if constexpr (NSTEP < 4) { WS_SP_DISPATCH(a.sp_mode, WS_DPPY_G4) }
             else return hipErrorInvalidValue;

@@ -207,9 +207,9 @@ ws_sim* sim_build(const ws_config_t* cfg, SlabInfo slab, ws::SlabComm* comm, hip
         }
         if (const char* e = env_str("WS_TB")) {
             s->tb = std::atoi(e);
-            // (4: where the kernel takes four steps -- Euler / RK2 on dppy, x2y in fp32 --
-            // else two: ws_sim::launch_tb)
-            require(s->tb == 1 || s->tb == 2 || s->tb == 4, WS_ERR_INVALID, "WS_TB must be 1, 2 or 4");
+            // (4 / 8: where the kernel takes them -- Euler / RK2 (8: Euler) on dppy, x2y in
+            // fp32 -- else the largest it takes: ws_sim::launch_tb)
+            require(s->tb == 1 || s->tb == 2 || s->tb == 4 || s->tb == 8, WS_ERR_INVALID, "WS_TB must be 1, 2, 4 or 8");
             require(!(s->kernel_env && ws::fused_split(s->kernel) && s->tb == 1), WS_ERR_INVALID,
                     "WS_KERNEL=pc / pc2 advance two steps per launch: WS_TB must be 2 (or unset)");
             s->tb_fixed = true;
@@ -920,8 +920,9 @@ int ws_sim_pin_variant(ws_sim_t* s, int32_t kernel, int32_t steps_per_launch, in
         require(s != nullptr, WS_ERR_INVALID, "null sim");
         require(kernel == -1 || kernel == kKernLds || ws::fused_is_dppy(kernel), WS_ERR_INVALID,
                 "kernel must be -1, WS_KERNEL_LDS, WS_KERNEL_DPPY, WS_KERNEL_X2Y, WS_KERNEL_PC or WS_KERNEL_PC2");
-        require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2 || steps_per_launch == 4,
-                WS_ERR_INVALID, "steps_per_launch must be -1, 1, 2 or 4");
+        require(steps_per_launch == -1 || steps_per_launch == 1 || steps_per_launch == 2 || steps_per_launch == 4 ||
+                    steps_per_launch == 8,
+                WS_ERR_INVALID, "steps_per_launch must be -1, 1, 2, 4 or 8");
         require(seg_rows == -1 || seg_rows > 0 || (chain_rounds(seg_rows) > 0 && chain_rounds(seg_rows) <= kMaxChainRounds),
                 WS_ERR_INVALID, "seg_rows must be -1, positive, or -2 .. -9 (chain schedule of 1 .. 8 rounds)");
         require(align == -1 || align == 0 || align == 1, WS_ERR_INVALID, "align must be -1, 0 or 1");

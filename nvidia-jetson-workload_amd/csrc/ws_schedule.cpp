@@ -392,12 +392,12 @@ bool config_spacing(const ws_sim* s) {
     return true;
 }
 
-// The largest launch (4, 2 or 1 steps) of at most `room` steps the tuned configuration
+// The largest launch (8, 4, 2 or 1 steps) of at most `room` steps the tuned configuration
 // allows: its steps per launch, and every step of a multi-step launch sees the config's
 // spacing (the kernel's later stages use it).
 static int launch_of(const ws_sim* s, int room) {
     if (room < 2 || !use_fused(s) || s->launch_tb() < 2 || !config_spacing(s)) return 1;
-    for (int k : {4, 2})
+    for (int k : {8, 4, 2})
         if (k <= s->launch_tb() && k <= room &&
             ws::fused_tb_ok(s->kernel, k, fused_stages(s), (int)elem_size(s->dtype)))
             return k;

@@ -357,7 +357,7 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
         if (ovl)
             for (ws_sim* s : gr->slabs) ensure_overlap_grids(s);
         for (int i = 0; i < k;) {
-            int n = 4;  // every slab must agree (they share the block position and the choice)
+            int n = 8;  // every slab must agree (they share the block position and the choice)
             for (ws_sim* s : gr->slabs) n = std::min(n, launch_steps(s, k - i));
             if (ovl) n = std::min(s0->block, k - i);
             if (ovl && s0->dtype == WS_F64) group_overlap_block<double>(gr, n, i == 0, i + n == k);

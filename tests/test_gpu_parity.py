@@ -58,12 +58,13 @@ def load(sim, s0):
 
 # (WS_FUSED, WS_KERNEL, WS_TB): every fused variant, dppy also with two steps per launch
 # (temporal blocking: run(n) advances pairs of steps per launch), and the per-stage kernels
-# (tb 4: four steps per launch where the kernel takes them -- Euler / RK2 on dppy, x2y in
-# fp32 -- two elsewhere)
-KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "dppy", "4"), ("1", "x2y", "1"), ("1", "x2y", "2"),
-           ("1", "x2y", "4"), ("1", "pc", "2"), ("1", "pc2", "2"), ("1", "lds", "1"), ("0", "x2y", "1")]
-KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_dppy_tb4", "fused_x2y", "fused_x2y_tb2", "fused_x2y_tb4",
-              "fused_pc_tb2", "fused_pc2_tb2", "fused_lds", "stage_kernels"]
+# (tb 4 / 8: four (eight: Euler) steps per launch where the kernel takes them -- dppy, x2y in
+# fp32 -- else the largest it takes)
+KERNELS = [("1", "dppy", "1"), ("1", "dppy", "2"), ("1", "dppy", "4"), ("1", "dppy", "8"), ("1", "x2y", "1"),
+           ("1", "x2y", "2"), ("1", "x2y", "4"), ("1", "x2y", "8"), ("1", "pc", "2"), ("1", "pc2", "2"),
+           ("1", "lds", "1"), ("0", "x2y", "1")]
+KERNEL_IDS = ["fused_dppy", "fused_dppy_tb2", "fused_dppy_tb4", "fused_dppy_tb8", "fused_x2y", "fused_x2y_tb2",
+              "fused_x2y_tb4", "fused_x2y_tb8", "fused_pc_tb2", "fused_pc2_tb2", "fused_lds", "stage_kernels"]
 # (kernel, steps per launch) of the fused variants
 FUSED = [("dppy", "1"), ("dppy", "2"), ("dppy", "4"), ("x2y", "1"), ("x2y", "2"), ("x2y", "4"), ("pc", "2"),
          ("pc2", "2"), ("lds", "1")]
@@ -521,21 +522,30 @@ def test_slab_group_levels_and_pe():
         np.testing.assert_array_equal(group.gather(name), one.get_current_grid()._get(name), err_msg=name)
 
 
-@pytest.mark.parametrize("kernel,fp64,method,want", [("x2y", False, 1, 4), ("dppy", False, 0, 4), ("dppy", True, 1, 4),
-                                                     ("x2y", True, 1, 2), ("dppy", False, 2, 2), ("pc", False, 1, 2)])
-def test_four_step_launches(kernel, fp64, method, want, monkeypatch):
-    """WS_TB=4: four steps per launch where the kernel takes them (Euler / RK2 on dppy, x2y in
-    fp32), two elsewhere; run(n) splits n into 4-, 2- and 1-step launches, and the result is
-    bit-for-bit the one-step run (ws_schedule.cpp launch_of)."""
+@pytest.mark.parametrize("kernel,fp64,method,pin,want", [("x2y", False, 1, 4, 4), ("dppy", False, 0, 4, 4),
+                                                         ("dppy", True, 1, 4, 4), ("x2y", True, 1, 4, 2),
+                                                         ("dppy", False, 2, 4, 2), ("pc", False, 1, 4, 2),
+                                                         ("x2y", False, 0, 8, 8), ("dppy", True, 0, 8, 8),
+                                                         ("dppy", True, 1, 8, 4)])
+def test_four_step_launches(kernel, fp64, method, pin, want, monkeypatch):
+    """WS_TB=4 / 8: four steps per launch where the kernel takes them (Euler / RK2 on dppy, x2y
+    in fp32), eight for Euler, else the largest it takes; run(n) splits n greedily into 8-, 4-,
+    2- and 1-step launches, and the result is bit-for-bit the one-step run (ws_schedule.cpp
+    launch_of)."""
     monkeypatch.setenv("WS_KERNEL", kernel)
-    monkeypatch.setenv("WS_TB", str(want if want == 4 else 4))
+    monkeypatch.setenv("WS_TB", str(pin))
     sim = make_sim(300, 83, 0, method, fp64)
     sim.set_initial_condition(ws.JetStreamInitialCondition())
     sim.initialize()
     assert sim.run(11) == 11
     assert sim.steps_per_launch() == want
     _, launches = sim.last_run_stats()
-    assert launches == (11 // 4 + 1 + 1 if want == 4 else 11 // 2 + 1)  # 4+4+2+1 / 2 x 5 + 1
+    expect, left = 0, 11
+    for k in (8, 4, 2, 1):
+        if k <= want:
+            expect += left // k
+            left %= k
+    assert launches == expect
     monkeypatch.setenv("WS_KERNEL", "dppy")
     monkeypatch.setenv("WS_TB", "1")
     ref = make_sim(300, 83, 0, method, fp64)

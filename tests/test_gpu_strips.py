@@ -39,9 +39,10 @@ def run_both(W, H, method, fp64, steps, dx=1.0, dy=2.0, f=0.3, align=None):
 
 
 @pytest.mark.parametrize("W", [2, 3, 7, 56, 57, 64, 120, 121, 127, 128, 129, 240, 241, 333])
-@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("dppy", "4"), ("x2y", "1"), ("x2y", "2"),
-                                      ("x2y", "4"), ("pc", "2"), ("pc2", "2")],
-                         ids=["dppy", "dppy_tb2", "dppy_tb4", "x2y", "x2y_tb2", "x2y_tb4", "pc_tb2", "pc2_tb2"])
+@pytest.mark.parametrize("kernel,tb", [("dppy", "1"), ("dppy", "2"), ("dppy", "4"), ("dppy", "8"), ("x2y", "1"),
+                                      ("x2y", "2"), ("x2y", "4"), ("x2y", "8"), ("pc", "2"), ("pc2", "2")],
+                         ids=["dppy", "dppy_tb2", "dppy_tb4", "dppy_tb8", "x2y", "x2y_tb2", "x2y_tb4", "x2y_tb8",
+                              "pc_tb2", "pc2_tb2"])
 @pytest.mark.parametrize("method", [0, 1, 2])
 @pytest.mark.parametrize("fp64", [False, True])
 def test_strip_widths(W, kernel, tb, method, fp64, monkeypatch):
