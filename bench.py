@@ -7,7 +7,9 @@ inputs resident in HBM. One "step" = one full time step of the whole grid, all N
 
   python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5] [--method rk4|rk2|euler]
 
-N > 1 (launched by torch.distributed.run, one process per GPU): the same global grid is
+N > 1 (one process per GPU: launched by torch.distributed.run, or -- with no launcher --
+bench.py starts torch.distributed.run with N ranks itself; a WORLD_SIZE other than --gpus is
+an error, exit status 2): the same global grid is
 y-slab decomposed over the ranks (strong scaling) and halo rows move over RCCL inside
 libws_hip.so. Timing: barrier + torch.cuda.synchronize() on both sides of exactly K steps,
 max over ranks. value = W*H*L*K / that time (whole job).
@@ -42,6 +44,11 @@ CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
 # cycles per instruction at 1 / 2 / 3 / 4 waves per SIMD, DPP moves 4.4 / 3.2 / 2.8 / 2.6 -- fp64
 # is not half rate here, and the fused kernels' limit is issue latency at their occupancy.
 VALU_CYC = 2
+# ... and the cycles a wave64 instruction of the fused march's mix (16 fp64 : 9 DPP) costs at the
+# occupancy it runs with (waves per SIMD -> SIMD cycles per instruction, the same probe): the
+# issue rate a latency-bound kernel can actually reach, so valu_frac_at_occupancy is the upper end
+# of the VALU utilisation range [valu_frac, valu_frac_at_occupancy]
+MIX_CYC_AT_WAVES = {1: 5.16, 2: 3.33, 3: 2.80, 4: 2.54}
 RAMP_S = 0.4           # untimed sustained load before the timed steps (DVFS clock ramp)
 
 CONFIGS = {
@@ -492,6 +499,42 @@ def bench_lpe(args, conf, method, world):
     print(json.dumps(result), flush=True)
 
 
+def launcher_command(n, argv, port):
+    """The torch.distributed.run command bench.py starts for `--gpus n` without a launcher:
+    one process per GPU of this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n, argv, runner=subprocess.call):
+    """Run bench.py under torch.distributed.run with n ranks as a child process (no GPU has
+    been touched in this process: a launcher must not be exec'd from a GPU process) and return
+    its exit status."""
+    cmd = launcher_command(n, argv, free_port())
+    log(f"--gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd)}")
+    return runner(cmd)
+
+
+def rank_count_check(gpus, env):
+    """(world size, error or None): the ranks of this launch must be exactly --gpus -- a
+    "multi-GPU" number must never silently come from fewer (or more) ranks."""
+    try:
+        world = int(env.get("WORLD_SIZE", "1"))
+    except ValueError:
+        return 1, f"WORLD_SIZE={env.get('WORLD_SIZE')!r} is not an integer"
+    if world != gpus:
+        return world, (f"--gpus {gpus} but this launch has WORLD_SIZE={world} ranks; launch with "
+                       f"--nproc-per-node {gpus}, or run without a launcher to let bench.py start them")
+    return world, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -505,15 +548,21 @@ def main():
                                                 "the variant a bench run chose)")
     args = ap.parse_args()
 
+    # --gpus N > 1 without a launcher: start N ranks ourselves -- torch.distributed.run as a
+    # fresh child process, before anything here touches the GPU -- and exit with its status
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    world, why = rank_count_check(args.gpus, os.environ)
+    if why:
+        log(f"error: {why}")
+        sys.exit(2)
+
     os.environ.setdefault("WS_QUIET", "1")
     import torch  # plumbing: contract timing (barrier + torch.cuda.synchronize); loaded before libws_hip
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("gloo")  # bootstrap (RCCL unique id) + host-side max over ranks
@@ -619,8 +668,16 @@ def main():
     # steps in between never leave the chip) -- the launch's compulsory HBM traffic
     compulsory = bpl / tb if variant != "stage_kernels" else bpl
     valu_frac = valu_insts * VALU_CYC / (SIMDS * CLOCK_HZ * launch_s) if valu_insts else None
+    waves = sim.kernel_occupancy()
+    occ_cyc = MIX_CYC_AT_WAVES.get(min(waves, 4)) if waves > 0 else None
+    valu_frac_occ = valu_insts * occ_cyc / (SIMDS * CLOCK_HZ * launch_s) if valu_insts and occ_cyc else None
     dram_frac = traffic / launch_s / 1e9 / HBM_PEAK_GBS if traffic else None
-    binding = None if valu_frac is None or dram_frac is None else "valu" if valu_frac > dram_frac else "hbm"
+    binding = None
+    if valu_frac is not None and dram_frac is not None:
+        hi = valu_frac_occ if valu_frac_occ is not None else valu_frac
+        # VALU utilisation is known only within [valu_frac, valu_frac_occ]: a DRAM fraction
+        # inside that range names no binding resource
+        binding = "hbm" if dram_frac > hi else "valu" if valu_frac > dram_frac else None
     achieved = compulsory / launch_s / 1e9
     result = {
         "metric": METRIC,
@@ -667,15 +724,21 @@ def main():
                      "valu_insts_per_launch": valu_insts,
                      "valu_f64_frac": f64_frac,
                      "valu_frac": valu_frac,
+                     "waves_per_simd": waves,
+                     "valu_frac_at_occupancy": valu_frac_occ,
                      "valu_model": f"SQ_INSTS_VALU per launch (PMC) x {VALU_CYC} issue cycles per wave64 "
                                    f"instruction on SIMD-32 (fp64 included: measured, tools/issue_probe.hip) / "
-                                   f"({SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz x mean launch time); valu_f64_frac = "
-                                   f"the fp64 share (PMC SQ_INSTS_VALU_{{ADD,MUL,FMA,TRANS}}_F64)",
+                                   f"({SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz x mean launch time); "
+                                   f"valu_frac_at_occupancy: the same at the kernel mix's measured issue cycles for "
+                                   f"its waves per SIMD ({MIX_CYC_AT_WAVES}, profiles/r04_issue_probe.txt); "
+                                   f"valu_f64_frac = the fp64 share (PMC SQ_INSTS_VALU_{{ADD,MUL,FMA,TRANS}}_F64)",
                      "binding": binding,
-                     "binding_note": (None if binding is None else
+                     "binding_note": (None if valu_frac is None or dram_frac is None else
+                                      "DRAM utilisation lies inside the VALU range [valu_frac, "
+                                      "valu_frac_at_occupancy]: no single binding resource" if binding is None else
                                       f"{binding} is the larger measured utilisation; below 0.7 neither HBM nor "
                                       f"VALU issue saturates (latency / occupancy bound)"
-                                      if max(valu_frac, dram_frac) < 0.7 else f"{binding}-bound"),
+                                      if max(valu_frac_occ or valu_frac, dram_frac) < 0.7 else f"{binding}-bound"),
                      "one_step_equivalent_gbs": bpl / launch_s / 1e9,
                      "one_step_equivalent_note": "6 words per cell-update x cell-updates per launch / launch time: "
                                                  "the HBM rate a one-step-per-launch kernel would need for this "

@@ -191,6 +191,10 @@ int ws_sim_synchronize(ws_sim_t* sim);
 /* Device milliseconds of the last ws_sim_run / ws_sim_run_until (hipEvents on the sim's
  * stream) and the number of stage kernels it launched. */
 int ws_sim_last_run_stats(const ws_sim_t* sim, double* device_ms, int64_t* kernel_launches);
+/* Test hook: the next ws_sim_run / ws_sim_step fails with WS_ERR_DEVICE right after its
+ * `after_launches`-th step launch (once; < 0 disarms) -- how the tests reach a run's error
+ * path (state left consistent: the completed launches' steps, time and PE T / P drift). */
+int ws_sim_inject_failure(ws_sim_t* sim, int32_t after_launches);
 
 /* ---- KernelAdapter plugin API (gpu_adaptability.hpp:242-329) --------------------- */
 /* One full forward-Euler step in -> out (the semantics of the reference's fused
@@ -244,6 +248,32 @@ int ws_group_create(const ws_config_t* cfg, int32_t nslabs, ws_group_t** out);
 int ws_group_destroy(ws_group_t* group);
 int ws_group_slab(ws_group_t* group, int32_t rank, ws_sim_t** sim, int32_t* row0, int32_t* rows);
 int ws_group_run(ws_group_t* group, int32_t num_steps, int32_t* steps_taken);
+
+/* Multi-GPU simulation in ONE process (new; the reference's WeatherSimulation
+ * takes one device, weather_sim.hpp:180): the y-slab decomposition of cfg's global grid over
+ * `ndevices` devices, slab r on devices[r]. Distinct devices: each slab is a full rank of the
+ * RCCL decomposition (exactly ws_sim_create_slab's, communicators created together), driven
+ * by a host thread of its own with its device current; ws_multi_run / _step / _run_until /
+ * _cfl run every rank at once. All devices equal (ndevices > 1): the slabs share that device
+ * and a slab group (device-copy halos) runs them. Slab handles (ws_multi_slab) are owned by
+ * the multi simulation: read / write their grids and query them, step only through ws_multi_*.
+ * Results are bitwise identical to one domain. */
+typedef struct ws_multi ws_multi_t;
+int ws_multi_create(const ws_config_t* cfg, const int32_t* devices, int32_t ndevices, ws_multi_t** out);
+int ws_multi_destroy(ws_multi_t* multi);
+/* *shared_device = 1 when the slabs share one device (slab group transport) */
+int ws_multi_size(const ws_multi_t* multi, int32_t* nslabs, int32_t* shared_device);
+int ws_multi_slab(ws_multi_t* multi, int32_t rank, ws_sim_t** sim, int32_t* row0, int32_t* rows);
+int ws_multi_step(ws_multi_t* multi);
+int ws_multi_run(ws_multi_t* multi, int32_t num_steps, int32_t* steps_taken);
+int ws_multi_run_until(ws_multi_t* multi, double max_time, int32_t* steps_taken);
+/* CFL of the global state (max over slabs; see ws_sim_cfl) */
+int ws_multi_cfl(ws_multi_t* multi, double* cfl, double* per_level, int32_t nlevels, double* ms);
+int ws_multi_synchronize(ws_multi_t* multi);
+/* After writing fields outside run() (an initial condition, field setters): refresh every
+ * slab's one-row u, v halo from its neighbours (collective) so vorticity / divergence read
+ * next are correct at the slab seams; run() does this itself at its end. */
+int ws_multi_exchange_diag_halo(ws_multi_t* multi);
 
 /* The halo exchange plan of rank `rank` (new; the reference has no distributed path): the
  * byte ranges a slab's exchange of `depth` rows of `nfields` level-stacked fields moves.
@@ -405,6 +435,9 @@ int ws_sim_slab_exchange_us(const ws_sim_t* sim, double* us);
  * must call it); per_level (optional, nlevels >= num_levels entries) = per level; ms
  * (optional) = device time of the reduction kernels. */
 int ws_sim_cfl(ws_sim_t* sim, double* cfl, double* per_level, int32_t nlevels, double* ms);
+/* Waves per SIMD one launch of the fused step kernel in use holds (hipOccupancy of the
+ * variant and steps per launch the autotuner chose; 0 for the per-stage kernels). */
+int ws_sim_kernel_occupancy(const ws_sim_t* sim, int32_t* waves_per_simd);
 
 /* ---- numerics mode of the fused step kernels ------------------------------------------
  * WS_NUMERICS_EXACT: the reference's arithmetic in the reference's evaluation order, no

@@ -36,10 +36,11 @@ struct FusedArgs {
     // spacing / numerics mode of the launch (SpacingMode below), set by the host
     int32_t sp_mode;
     // Chain schedule (dppy / x2y / pc / pc2; nullptr = the segments above): workgroup w marches
-    // chains[w] -- one long segment per workgroup, sized by the host so that every march of a
-    // round costs the same (edge strips / segments run the dearer clamped code) and a round is
-    // exactly the workgroups the chip holds at once: no round of short-lived waves to quantise,
-    // one warm-up per chain. seg_rows then holds the longest chain's rows.
+    // chains[w] -- one long segment per workgroup, sized by the host (ws_schedule.cpp
+    // chain_table) so that every chain of a launch costs the same (edge strips / segments run
+    // the dearer clamped code), with r chains per SIMD (r x 4 x CUs waves in all, whatever the
+    // kernel's occupancy): no round of short-lived waves to quantise, one warm-up per chain.
+    // seg_rows then holds the longest chain's rows.
     const ChainSeg* chains;
     int32_t nchains;
 };

@@ -127,7 +127,8 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     // 2 cone + 48 rows of pitch below 2^31 bytes; C5's 16384-row strips at one chain per strip)
     const int64_t row_bytes = (int64_t)g->pitch * (int64_t)elem_size(s->dtype);
     // (nine tenths of it: the y-edge weights below lengthen the other chains of a group a little)
-    const int max_rows = (int)std::max<int64_t>(min_rows, (0x7fffffff / row_bytes - 2 * cone - 64) * 9 / 10);
+    const int64_t span_rows = 0x7fffffff / row_bytes - 2 * cone - 49;  // longest chain the launcher takes
+    const int max_rows = (int)std::max<int64_t>(min_rows, span_rows * 9 / 10);
     auto floor_n = [&](const Group& gr) { return (gr.r.rows() + max_rows - 1) / max_rows; };
     int64_t assigned = 0;
     for (Group& gr : groups) {
@@ -148,9 +149,8 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     auto yclamped = [&](int y0, int y1) { return (g->top_clamp && y0 < cone) || (g->bot_clamp && y1 > g->H - cone); };
     std::vector<std::vector<ws::ChainSeg>> per(groups.size());
     int maxn = 0;
-    for (size_t gi = 0; gi < groups.size(); ++gi) {
-        const Group& gr = groups[gi];
-        const int rows = gr.r.rows(), n = gr.n;
+    auto split = [&](const Group& gr, int n) {
+        const int rows = gr.r.rows();
         const bool top = yclamped(gr.r.y0, gr.r.y0 + 1), bot = yclamped(gr.r.y1 - 1, gr.r.y1);
         // weights of the first / last chain (y-clamped ones are dearer per row)
         std::vector<double> w(n, 1.0);
@@ -158,6 +158,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
         if (bot) w[n - 1] = n == 1 ? std::max(w[n - 1], kYClampCost) : kYClampCost;
         double inv = 0;
         for (double x : w) inv += 1.0 / x;
+        std::vector<ws::ChainSeg> out;
         int y = gr.r.y0;
         double acc = 0;
         for (int c = 0; c < n; ++c) {
@@ -165,10 +166,21 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
             int y1 = c == n - 1 ? gr.r.y1 : gr.r.y0 + (int)std::lround(acc);
             y1 = std::max(y1, y + 1);
             y1 = std::min(y1, gr.r.y1 - (n - 1 - c));  // leave a row for every later chain
-            per[gi].push_back(ws::ChainSeg{gr.unit, y, y1, 0});
+            out.push_back(ws::ChainSeg{gr.unit, y, y1, 0});
             y = y1;
         }
-        maxn = std::max(maxn, n);
+        return out;
+    };
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        // the edge weights lengthen a group's other chains: one more chain until every chain
+        // fits the descriptor span
+        for (int n = groups[gi].n;; ++n) {
+            per[gi] = split(groups[gi], n);
+            bool fits = true;
+            for (const ws::ChainSeg& cs : per[gi]) fits = fits && cs.y1 - cs.y0 <= span_rows;
+            if (fits) break;
+        }
+        maxn = std::max(maxn, (int)per[gi].size());
     }
     // table order: chain position, then unit -- neighbouring strips at the same rows adjacent
     ws_sim::ChainTable t;
@@ -181,6 +193,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
                 t.max_rows = std::max(t.max_rows, per[gi][c].y1 - per[gi][c].y0);
             }
     t.n = (int32_t)tab.size();
+    require(t.max_rows <= span_rows, WS_ERR_INVALID, "chain longer than a buffer descriptor spans");
     WS_HIP_CHECK(hipMalloc(&t.dev, tab.size() * sizeof(ws::ChainSeg)));
     WS_HIP_CHECK(hipMemcpy(t.dev, tab.data(), tab.size() * sizeof(ws::ChainSeg), hipMemcpyHostToDevice));
     s->chain_tables.push_back(t);
@@ -232,6 +245,24 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     else WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(s->kernel, nst, nsteps, a, g, st));
     ++s->last_launches;
 }
+
+// Waves per SIMD the chosen fused variant's launches hold (hipOccupancy of the instantiation a
+// tb-step launch runs; 0 for the per-stage kernels / fused_lds): what the VALU issue rate of the
+// march depends on (bench.py prices VALU issue cycles by it).
+template <typename T>
+int fused_waves_per_simd(const ws_sim* s) {
+    if (!use_fused(s) || s->kernel == kKernLds) return 0;
+    ws::FusedArgs<T> a{};
+    a.c_dt = (T)s->dt;
+    a.sp1 = make_spacing<T>(s->slot[s->cur]->dx, s->slot[s->cur]->dy);
+    a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
+    if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
+    else a.sp_mode = ws::exact_sp_mode(a);
+    const int wgs = ws::fused_dppy_blocks_per_cu<T>(s->kernel, fused_stages(s), s->launch_tb(), a.sp_mode);
+    return wgs * (ws::fused_split(s->kernel) ? 2 : 1) / 4;
+}
+template int fused_waves_per_simd<float>(const ws_sim*);
+template int fused_waves_per_simd<double>(const ws_sim*);
 
 // Phase 1 of a step: everything that does not need this step's halo rows.
 //  * single domain: the whole step (fused or stage kernels);
@@ -606,17 +637,29 @@ void run_steps(ws_sim* s, int k) {
         }
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
-        // the T / P drift of the whole run in one pass at its end (tp_flush); a run that threw
-        // before its flush leaves its completed launches' drift to apply first
-        if (s->tp_lazy) {
-            if (s->dtype == WS_F64) tp_flush<double>(s);
-            else tp_flush<float>(s);
-        }
+        // the T / P drift of the whole run in one pass at its end (tp_flush; on a throw, the
+        // guard below applies the completed launches' drift before the error leaves run())
         s->tp_lazy = true;
         s->tp_steps = 0;
         s->tp_src[0] = s->slot[s->cur]->f[WS_FIELD_T];
         s->tp_src[1] = s->slot[s->cur]->f[WS_FIELD_P];
     }
+    // A run that throws after some launches (a HIP / RCCL error) must not leave the T / P drift
+    // pending: T / P would lag u, v, h, and a later flush would overwrite fields reset or set in
+    // between. The guard flushes what the completed launches owe (normal exits flushed already).
+    struct TpGuard {
+        ws_sim* s;
+        ~TpGuard() {
+            if (!s->tp_lazy) return;
+            try {
+                if (s->dtype == WS_F64) tp_flush<double>(s);
+                else tp_flush<float>(s);
+            } catch (...) {
+            }
+            s->tp_lazy = false;
+            s->tp_steps = 0;
+        }
+    } tp_guard{s};
     // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
     // schedule's blocks (edge bands + exchange on the edge stream, interior on the compute stream)
     // (marks: events recorded on the compute stream after the first block and after the last)
@@ -637,6 +680,10 @@ void run_steps(ws_sim* s, int k) {
             for (int j = 0; j < n; ++j) {
                 s->time = advance_time(s, s->time);
                 s->step++;
+            }
+            if (s->fail_after >= 0 && s->last_launches >= s->fail_after) {  // ws_sim_inject_failure (tests)
+                s->fail_after = -1;
+                throw WsError(WS_ERR_DEVICE, "injected failure after a launch (ws_sim_inject_failure)");
             }
             const int prev = i;
             i += n;

@@ -179,6 +179,7 @@ struct ws_sim {
     int64_t tp_steps = 0;
     int tp_last = 0;
     void* tp_src[2] = {nullptr, nullptr};
+    int64_t fail_after = -1;  // test hook (ws_sim_inject_failure): throw once this many launches ran
     double last_ms = 0.0;
     int64_t last_launches = 0;
     ws::KernelTimer timer;
@@ -276,6 +277,8 @@ void step_begin(ws_sim* s, int nsteps = 1);
 template <typename T>
 void step_end(ws_sim* s, int nsteps = 1);
 int launch_steps(const ws_sim* s, int remaining);
+template <typename T>
+int fused_waves_per_simd(const ws_sim* s);  // occupancy of the chosen fused variant (0: none)
 // overlap schedule pieces (the slab group runs them per slab, ws_slab.cpp)
 bool overlap_active(const ws_sim* s);
 void ensure_overlap_grids(ws_sim* s);
@@ -289,6 +292,9 @@ void slab_exchange(ws_sim* s, ws_grid* g, int nfields, int depth, hipStream_t st
 double advance_time(const ws_sim* s, double t);  // t + dt in the simulation's precision
 int plan_steps(const ws_sim* s, int n);          // steps run(n) takes (max_time cap)
 void run_steps(ws_sim* s, int k);
+
+// ---- ws_slab.cpp ----
+void group_diag_halo(ws_group* gr);  // one-row u, v halos of every slab (diagnostics at seams)
 
 // ---- ws_autotune.cpp ----
 void autotune(ws_sim* s);  // variant choice at the first run (cache, timing, rank-0 broadcast)

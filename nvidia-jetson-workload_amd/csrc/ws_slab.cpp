@@ -276,6 +276,16 @@ void group_step(ws_group* gr, int nsteps) {
     for (ws_sim* s : gr->slabs) step_end<T>(s, nsteps);
 }
 
+// After field writes outside run() (initial conditions, setters): every slab's one-row u, v
+// halo from its neighbours, so diagnostics read next see the neighbours' current rows at the
+// seams (run() refreshes it at its end, see run_steps)
+void group_diag_halo(ws_group* gr) {
+    set_device(gr->device);
+    group_exchange(gr, 2, 1);
+    for (ws_sim* s : gr->slabs) s->slot[s->cur]->diag_pending = true;
+    WS_HIP_CHECK(hipStreamSynchronize(gr->stream));
+}
+
 }  // namespace wsr
 
 extern "C" {

@@ -11,6 +11,8 @@ from .weather_simulation import (  # noqa: F401
     InitialCondition, InitialConditionFactory, IntegrationMethod, JetStreamInitialCondition, KernelAdapter,
     KernelAdapterFactory, MountainInitialCondition, OutputConfig, OutputFormat, OutputManager, PerformanceMetrics,
     SlabGroup,
+    MultiGPUSimulation,
+    SlabbedGrid,
     RandomInitialCondition, SimulationConfig, SimulationModel, UniformInitialCondition, VortexInitialCondition,
     WeatherGrid, WeatherSimulation, WeatherSimulationWrapper, ZonalFlowInitialCondition, create_initial_condition,
     get_available_initial_conditions, get_device_info, is_cuda_available, register_all_initial_conditions)

@@ -104,6 +104,7 @@ SIGNATURES = {
     "ws_sim_reset_metrics": [_P],
     "ws_sim_synchronize": [_P],
     "ws_sim_last_run_stats": [_P, _PD, _PL],
+    "ws_sim_inject_failure": [_P, _I],
     "ws_adapter_execute_shallow_water_step": [_P, _P, _D, _D, _D, _PD],
     "ws_adapter_execute_barotropic_step": [_P, _P, _D, _D, _D, _PD],
     "ws_adapter_execute_primitive_equations_step": [_P, _P, _D, _D, _D, _PD],
@@ -124,12 +125,23 @@ SIGNATURES = {
     "ws_group_destroy": [_P],
     "ws_group_slab": [_P, _I, _PP, _PI, _PI],
     "ws_group_run": [_P, _I, _PI],
+    "ws_multi_create": [ctypes.POINTER(ws_config_t), _PI, _I, _PP],
+    "ws_multi_destroy": [_P],
+    "ws_multi_size": [_P, _PI, _PI],
+    "ws_multi_slab": [_P, _I, _PP, _PI, _PI],
+    "ws_multi_step": [_P],
+    "ws_multi_run": [_P, _I, _PI],
+    "ws_multi_run_until": [_P, _D, _PI],
+    "ws_multi_cfl": [_P, _PD, _PD, _I, _PD],
+    "ws_multi_synchronize": [_P],
+    "ws_multi_exchange_diag_halo": [_P],
     "ws_sim_set_kernel_timing": [_P, _I],
     "ws_sim_kernel_timing": [_P, _I, _PL, _PD, _PD],
     "ws_sim_fused_variant": [_P, _PI, _PI, _PI],
     "ws_sim_steps_per_launch": [_P, _PI],
     "ws_sim_slab_schedule": [_P, _PI, _PI],
     "ws_sim_cfl": [_P, _PD, _PD, _I, _PD],
+    "ws_sim_kernel_occupancy": [_P, _PI],
     "ws_sim_set_numerics": [_P, _I],
     "ws_sim_get_numerics": [_P, _PI],
     "ws_slab_exchange_plan": [_I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ws_xfer_t), _I, _PI, _PL, _PL],

@@ -10,9 +10,9 @@ in include/ws_hip.h). There is no CPU compute path and no mock fallback.
 Deliberate deviations from the reference (documented in DESIGN.md):
   * ComputeBackend CUDA / Hybrid / AdaptiveHybrid run the HIP path (the reference runs
     every backend through its CPU solver; its CUDA branch was an empty placeholder,
-    weather_simulation.cpp:492-500, 562-591). ComputeBackend.CPU (backend="cpu") is refused
-    with NotImplementedError: this build has no CPU compute path, and silently running the
-    GPU under that name would misreport where the work ran.
+    weather_simulation.cpp:492-500, 562-591). ComputeBackend.CPU (backend="cpu") runs the
+    HIP path too, with a one-time RuntimeWarning saying so: this build has no CPU solver, and
+    the HIP results are the CPU solver's bits.
   * SimulationConfig.double_precision is honoured (fp64 grids); fp32 is the default and
     matches the reference bit-for-bit.
   * num_levels > 1 stores [L, H, W] fields of independent 2-D levels (the reference
@@ -24,6 +24,7 @@ import ctypes
 import os
 import random
 import time
+import warnings
 from enum import IntEnum
 from typing import Dict, List, Optional, Union
 
@@ -127,6 +128,9 @@ class SimulationConfig:
         self.output_interval = 10
         self.output_path = "./output"
         self.random_seed = random.SystemRandom().getrandbits(32)  # std::random_device{}()
+        # extension: HIP device ids of a one-process multi-GPU run -- more than
+        # one makes WeatherSimulation(config) a MultiGPUSimulation (one y-slab per device)
+        self.devices = None
 
     def _to_c(self):
         c = _native.ws_config_t()
@@ -386,8 +390,10 @@ class InitialCondition:
 
     def initialize(self, grid: WeatherGrid, level: Optional[int] = None):
         arr = (ctypes.c_double * max(1, len(self._params)))(*self._params)
-        check(lib.ws_grid_apply_initial_condition(grid._h, self._ws_name.encode(), arr, len(self._params),
-                                                  self._sparam.encode(), -1 if level is None else int(level)))
+        # a multi-GPU grid (SlabbedGrid): every slab in global coordinates, its own rows
+        for g in getattr(grid, "slab_grids", None) or [grid]:
+            check(lib.ws_grid_apply_initial_condition(g._h, self._ws_name.encode(), arr, len(self._params),
+                                                      self._sparam.encode(), -1 if level is None else int(level)))
 
     def get_name(self):
         return self._ws_name
@@ -517,7 +523,26 @@ _BACKEND_NAMES = {0: "HIP GPU (MI355X)", 1: "HIP GPU (MI355X; CPU requested)", 2
                   3: "HIP GPU (MI355X; adaptive hybrid requested)"}
 
 
+_CPU_WARNED = []
+
+
+def _warn_cpu_backend(config):
+    """ComputeBackend.CPU runs the HIP kernels (no CPU solver in this build): say so, once."""
+    if int(config.compute_backend) == int(ComputeBackend.CPU) and not _CPU_WARNED:
+        _CPU_WARNED.append(True)
+        warnings.warn("ComputeBackend.CPU requested: libws_hip has no CPU solver, the HIP kernels run on the GPU "
+                      "instead (results bit-identical to the reference CPU solver in fp32 / exact fp64)",
+                      RuntimeWarning, stacklevel=3)
+
+
 class WeatherSimulation:
+    def __new__(cls, config=None, *args, **kw):
+        # config.devices with more than one device: the one-process multi-GPU simulation
+        if (cls is WeatherSimulation and not args and not kw and config is not None
+                and len(getattr(config, "devices", None) or ()) > 1):
+            return super().__new__(MultiGPUSimulation)
+        return super().__new__(cls)
+
     def __init__(self, config: SimulationConfig, _slab=None, _handle=None, _owner=None):
         self._config_py = config
         self._owner = _owner
@@ -549,6 +574,7 @@ class WeatherSimulation:
                                              ctypes.byref(r0), ctypes.byref(nr)))
             self.row0, self.rows = r0.value, nr.value
         self._h = h
+        _warn_cpu_backend(config)
         _say(f"Using compute backend: {_BACKEND_NAMES.get(int(config.compute_backend), 'HIP GPU (MI355X)')}")
 
     def __del__(self):
@@ -701,6 +727,13 @@ class WeatherSimulation:
         out = (c.value, arr) if per_level else c.value
         return (out, ms.value) if with_time else out
 
+    def kernel_occupancy(self):
+        """Extension: waves per SIMD a launch of the fused step kernel in use holds (ws_hip.h
+        ws_sim_kernel_occupancy; 0 for the per-stage kernels)."""
+        n = ctypes.c_int32()
+        check(lib.ws_sim_kernel_occupancy(self._h, ctypes.byref(n)))
+        return n.value
+
     def steps_per_launch(self):
         """Extension: time steps one fused launch advances inside run() (1, or 2 / 4 with
         temporal blocking; ws_hip.h ws_sim_steps_per_launch)."""
@@ -818,6 +851,183 @@ class SlabGroup:
         a = np.asarray(arr)
         for s in self._slabs:
             s.get_current_grid()._set(name, a[..., s.row0:s.row0 + s.rows, :])
+
+
+class SlabbedGrid(WeatherGrid):
+    """Extension: the global view of one grid slot of a y-slab decomposition (a
+    MultiGPUSimulation's current grid). Field reads assemble the (H, W) / (L, H, W) array
+    from the slabs' owned rows, writes scatter it; `slab_grids` are the per-slab grids."""
+
+    def __init__(self, grids, owner):
+        self._owner = owner
+        self._owned = False
+        self._h = None
+        self.slab_grids = list(grids)
+        g0 = self.slab_grids[0]
+        self._W, self._L, self._dtype, self._ws_dtype = g0._W, g0._L, g0._dtype, g0._ws_dtype
+        self._rows, r0 = [], 0
+        for g in self.slab_grids:
+            self._rows.append((r0, g._H))
+            r0 += g._H
+        self._H = r0
+
+    def reset(self):
+        for g in self.slab_grids:
+            g.reset()
+
+    def get_dx(self):
+        return self.slab_grids[0].get_dx()
+
+    def get_dy(self):
+        return self.slab_grids[0].get_dy()
+
+    def set_spacing(self, dx, dy):
+        for g in self.slab_grids:
+            g.set_spacing(dx, dy)
+
+    def calculate_diagnostics(self):
+        for g in self.slab_grids:
+            g.calculate_diagnostics()
+
+    def _get(self, name, level=None):
+        return np.concatenate([g._get(name, level) for g in self.slab_grids], axis=-2)
+
+    def _set(self, name, arr, level=None):
+        a = np.asarray(arr)
+        if a.ndim not in (2, 3):
+            raise RuntimeError("Number of dimensions must be 2")
+        if a.shape[-2:] != (self._H, self._W):
+            raise RuntimeError("Array dimensions must match field dimensions")
+        for g, (r0, n) in zip(self.slab_grids, self._rows):
+            g._set(name, a[..., r0:r0 + n, :], level)
+        if name in ("u", "v") and self._owner is not None:
+            self._owner._diag_halo()  # seam diagnostics read the neighbours' new rows
+
+    def device_field(self, name):
+        raise NotImplementedError("a multi-GPU grid has one device field per slab: use slab_grids[r].device_field")
+
+
+class MultiGPUSimulation(WeatherSimulation):
+    """Extension: ONE simulation object over several GPUs of one process --
+    `WeatherSimulation(config)` with `config.devices = [0, 1, ...]`, or
+    `MultiGPUSimulation(config, devices=[...])`. The global grid is y-slab decomposed, slab r
+    on devices[r]; distinct devices exchange halo rows over RCCL (xGMI), each slab driven by a
+    host thread of the library (ws_hip.h ws_multi_*), all-equal devices share one GPU through
+    device copies. The API is the single-domain one: run / step / run_until, the current
+    grid's fields as global arrays, bitwise identical to one domain (and the reference)."""
+
+    def __init__(self, config: SimulationConfig, devices=None):
+        self._config_py = config
+        self._owner = None
+        self._ic = None
+        self._om = None
+        self._owned = False  # the slabs belong to the multi simulation (ws_multi_destroy)
+        devices = [int(d) for d in (config.devices if devices is None else devices)]
+        if not devices:
+            raise ValueError("MultiGPUSimulation needs at least one device")
+        arr = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        check(lib.ws_multi_create(ctypes.byref(config._to_c()), arr, len(devices), ctypes.byref(h)))
+        self._m = h
+        self.devices = devices
+        n, shared = ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_multi_size(self._m, ctypes.byref(n), ctypes.byref(shared)))
+        self.shared_device = bool(shared.value)
+        self._slabs = []
+        for r in range(n.value):
+            s, r0, nr = ctypes.c_void_p(), ctypes.c_int32(), ctypes.c_int32()
+            check(lib.ws_multi_slab(self._m, r, ctypes.byref(s), ctypes.byref(r0), ctypes.byref(nr)))
+            self._slabs.append(WeatherSimulation(config, _slab=(r0.value, nr.value), _handle=s.value, _owner=self))
+        self._h = self._slabs[0]._h  # per-slab state every slab shares (time, step, dt, variant) is read here
+        self.row0, self.rows = 0, config.grid_height
+        _warn_cpu_backend(config)
+        _say(f"Using compute backend: HIP GPU (MI355X) x {len(devices)} "
+             f"({'one device, device-copy halos' if self.shared_device else 'RCCL halos'})")
+
+    def __del__(self):
+        if getattr(self, "_m", None):
+            self._slabs = []
+            lib.ws_multi_destroy(self._m)
+            self._m = None
+
+    @property
+    def nslabs(self):
+        return len(self._slabs)
+
+    def slab(self, rank):
+        """Rank `rank`'s slab (a WeatherSimulation view of rows [row0, row0 + rows))."""
+        return self._slabs[rank]
+
+    def initialize(self):
+        for s in self._slabs:
+            check(lib.ws_sim_initialize(s._h))
+        if self._ic is not None:
+            self._ic.initialize(self.get_current_grid())
+        self._diag_halo()
+        if self._om is not None:
+            self._om.initialize(self)
+
+    def _diag_halo(self):
+        check(lib.ws_multi_exchange_diag_halo(self._m))
+
+    def step(self):
+        check(lib.ws_multi_step(self._m))
+
+    def _run_native(self, n):
+        taken = ctypes.c_int32()
+        check(lib.ws_multi_run(self._m, int(n), ctypes.byref(taken)))
+        return taken.value
+
+    def run_until(self, max_time):
+        if self._om is not None:
+            return super().run_until(max_time)
+        taken = ctypes.c_int32()
+        check(lib.ws_multi_run_until(self._m, float(max_time), ctypes.byref(taken)))
+        return taken.value
+
+    def set_dt(self, dt):
+        for s in self._slabs:
+            s.set_dt(dt)
+
+    def get_current_grid(self):
+        return SlabbedGrid([s.get_current_grid() for s in self._slabs], self)
+
+    def reset_performance_metrics(self):
+        for s in self._slabs:
+            s.reset_performance_metrics()
+
+    def synchronize(self):
+        check(lib.ws_multi_synchronize(self._m))
+
+    def set_kernel_timing(self, enable=True, reserve=0):
+        for s in self._slabs:
+            s.set_kernel_timing(enable, reserve)
+
+    def get_cfl(self, per_level=False, with_time=False):
+        c, ms = ctypes.c_double(), ctypes.c_double()
+        arr = np.empty(max(1, int(self._config_py.num_levels)), np.float64)
+        check(lib.ws_multi_cfl(self._m, ctypes.byref(c), arr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), arr.size,
+                               ctypes.byref(ms)))
+        out = (c.value, arr) if per_level else c.value
+        return (out, ms.value) if with_time else out
+
+    def set_slab_schedule(self, block=0, overlap="auto"):
+        for s in self._slabs:
+            s.set_slab_schedule(block, overlap)
+
+    def pin_variant(self, **kw):
+        for s in self._slabs:
+            s.pin_variant(**kw)
+
+    def set_numerics(self, mode):
+        for s in self._slabs:
+            s.set_numerics(mode)
+
+    def comm_allreduce_max(self, value):
+        return float(value)  # one process holds every rank
+
+    def comm_barrier(self):
+        self.synchronize()
 
 
 # ---------------------------------------------------------------------------------
@@ -1029,12 +1239,12 @@ _SNAPSHOT = (
 class WeatherSimulationWrapper:
     """High-level wrapper: string arguments, lazy initialisation and periodic snapshots
     around one WeatherSimulation (same constructor signature and defaults as the reference,
-    plus double_precision / num_levels)."""
+    plus double_precision / num_levels, and devices=[...] for one simulation over several GPUs)."""
 
     def __init__(self, width: int = 256, height: int = 256, model: Union[str, int] = "shallow_water", dt: float = 0.01,
                  integration_method: Union[str, int] = "rk4", backend: Union[str, int] = "adaptive",
                  device_id: int = 0, threads: int = 0, output_interval: int = 10, output_path: str = "./output",
-                 double_precision: bool = False, num_levels: int = 1):
+                 double_precision: bool = False, num_levels: int = 1, devices: Optional[List[int]] = None):
         cfg = SimulationConfig()
         for field, value in (("grid_width", width), ("grid_height", height), ("dt", dt),
                              ("output_interval", output_interval), ("output_path", output_path),
@@ -1044,6 +1254,7 @@ class WeatherSimulationWrapper:
                              ("integration_method", _enum_arg("integration_method", integration_method)),
                              ("compute_backend", _enum_arg("compute_backend", backend))):
             setattr(cfg, field, value)
+        cfg.devices = list(devices) if devices else None  # extension: > 1 device = MultiGPUSimulation
         self.config = cfg
         self.simulation = WeatherSimulation(cfg)
         self.initialized = False

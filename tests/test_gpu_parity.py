@@ -558,6 +558,52 @@ def test_four_step_launches(kernel, fp64, method, pin, want, monkeypatch):
 
 
 @pytest.mark.parametrize("tb", ["1", "2", "4"])
+@pytest.mark.parametrize("fail_after", [1, 2])
+def test_pe_drift_on_a_failed_run(fail_after, tb, monkeypatch):
+    """A run that fails after some launches (ws_sim_inject_failure) leaves a consistent state:
+    T / P carry exactly the drift of the steps the completed launches took (== that many
+    step() calls, bit for bit), and nothing pending lands later -- neither on a following run
+    nor on fields reset by initialize()."""
+    monkeypatch.setenv("WS_KERNEL", "x2y")
+    monkeypatch.setenv("WS_TB", tb)
+    sims = []
+    for _ in range(3):
+        sim = make_sim(200, 72, 2, 1, False, levels=3, max_time=1e30)
+        sim.set_initial_condition(ws.JetStreamInitialCondition())
+        sim.initialize()
+        sims.append(sim)
+    a, b, c = sims
+    assert a.run(2) == 2
+    ws._native.check(ws._native.lib.ws_sim_inject_failure(a._h, fail_after))
+    with pytest.raises(ws._native.WsDeviceError, match="injected"):
+        a.run(11)
+    k = a.get_current_step()
+    assert 2 < k < 13
+    for _ in range(k):
+        b.step()
+    assert b.get_current_time() == a.get_current_time()
+    ga, gb = a.get_current_grid(), b.get_current_grid()
+    for get in ("get_temperature_field", "get_pressure_field", "get_height_field", "get_velocity_field"):
+        np.testing.assert_array_equal(getattr(ga, get)(), getattr(gb, get)(), err_msg=get)
+    # a later run continues from there exactly
+    assert a.run(5) == 5
+    for _ in range(5):
+        b.step()
+    for get in ("get_temperature_field", "get_pressure_field", "get_height_field"):
+        np.testing.assert_array_equal(getattr(a.get_current_grid(), get)(), getattr(b.get_current_grid(), get)(),
+                                      err_msg=get)
+    # a failed run followed by initialize(): no drift of the failed run reaches the reset fields
+    ws._native.check(ws._native.lib.ws_sim_inject_failure(a._h, fail_after))
+    with pytest.raises(ws._native.WsDeviceError):
+        a.run(9)
+    a.initialize()
+    assert a.run(4) == c.run(4) == 4
+    for get in ("get_temperature_field", "get_pressure_field", "get_height_field"):
+        np.testing.assert_array_equal(getattr(a.get_current_grid(), get)(), getattr(c.get_current_grid(), get)(),
+                                      err_msg=get)
+
+
+@pytest.mark.parametrize("tb", ["1", "2", "4"])
 @pytest.mark.parametrize("k", [1, 3, 7, 12])
 def test_pe_drift_once_per_run(k, tb, monkeypatch):
     """PE T / P: run(k) applies the k steps' drift in one pass at its end (ws_schedule.cpp
@@ -577,3 +623,26 @@ def test_pe_drift_once_per_run(k, tb, monkeypatch):
     a, b = sims[0].get_current_grid(), sims[1].get_current_grid()
     for get in ("get_temperature_field", "get_pressure_field", "get_height_field"):
         np.testing.assert_array_equal(getattr(a, get)(), getattr(b, get)(), err_msg=get)
+
+
+def test_cpu_backend_runs_hip_with_one_warning(monkeypatch):
+    """ComputeBackend.CPU (the reference's own tests request it) runs the HIP path:
+    same bits as the CUDA backend, and one RuntimeWarning per process saying so (D8)."""
+    from weather_sim import weather_simulation as wsm
+    monkeypatch.setattr(wsm, "_CPU_WARNED", [])
+    out = []
+    for backend in (ws.ComputeBackend.CUDA, ws.ComputeBackend.CPU, ws.ComputeBackend.CPU):
+        c = ws.SimulationConfig()
+        c.grid_width, c.grid_height = 64, 48
+        c.compute_backend = backend
+        import warnings
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            sim = ws.WeatherSimulation(c)
+        out.append(sum(issubclass(w.category, RuntimeWarning) and "CPU" in str(w.message) for w in rec))
+        sim.set_initial_condition(ws.VortexInitialCondition())
+        sim.initialize()
+        sim.run(7)
+        out.append(sim.get_current_grid().get_height_field())
+    assert out[0] == 0 and out[2] == 1 and out[4] == 0
+    assert np.array_equal(out[1], out[3]) and np.array_equal(out[1], out[5])
