@@ -90,13 +90,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def _new_uid(native):
-    import ctypes
-    buf = (ctypes.c_uint8 * native.COMM_ID_BYTES)()
-    native.check(native.lib.ws_comm_get_unique_id(buf))
-    return bytes(buf)
-
-
 def bootstrap_uid(dist, rank, make_uid, nbytes=128):
     """Rank 0 creates the RCCL unique id; every rank receives it over the (gloo) host group."""
     import torch
@@ -568,7 +561,6 @@ def main():
         dist.init_process_group("gloo")  # bootstrap (RCCL unique id) + host-side max over ranks
 
     import weather_sim as ws
-    from weather_sim import _native
 
     conf = CONFIGS[args.config]
     method = METHODS[args.method]
@@ -584,9 +576,9 @@ def main():
     cfg.device_id = local
     cfg.max_time = 1e30  # run() would otherwise stop at t >= 10 (1000 steps of dt = 0.01)
 
-    if world > 1:
-        uid = bootstrap_uid(dist, rank, lambda: _new_uid(_native))
-        sim = ws.WeatherSimulation(cfg, _slab=(rank, world, uid))
+    if world > 1:  # one rank of the decomposition over processes (weather_sim.SlabSimulation)
+        uid = bootstrap_uid(dist, rank, ws.new_comm_id)
+        sim = ws.SlabSimulation(cfg, rank, world, uid)
     else:
         sim = ws.WeatherSimulation(cfg)
 

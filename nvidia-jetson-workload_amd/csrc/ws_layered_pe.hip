@@ -64,9 +64,9 @@ __device__ __forceinline__ int wrapi(int i, int n) { return i < 0 ? i + n : (i >
 #define WS_LPE_CHUNK 8
 #endif
 constexpr int kChunk = WS_LPE_CHUNK;
-#ifndef WS_LPE_UNROLL
-#define WS_LPE_UNROLL 1  // 1024^2 x 32 fp32 RK4: 32x8 tile 1 / 2 / 4 / 8 -> 15.2 / 16.2 / 14.2 / 15.5; 128x8 tile 1 / 2 -> 18.8 / 17.6 Gcell/s
-#endif
+// the level walk is not unrolled (`#pragma unroll 1` below; a literal: -save-temps does not
+// expand macros inside pragmas): 1024^2 x 32 fp32 RK4: 32x8 tile 1 / 2 / 4 / 8 -> 15.2 / 16.2 /
+// 14.2 / 15.5; 128x8 tile 1 / 2 -> 18.8 / 17.6 Gcell/s
 constexpr int kColsPerThread = (kCX * kCY + kTX * kTY - 1) / (kTX * kTY);
 
 #ifndef WS_LPE_HLDS
@@ -152,7 +152,7 @@ void lpe_stage_kernel(LpeArgs<T> a) {
         }
         __syncthreads();
         if (inside) {
-#pragma unroll WS_LPE_UNROLL
+#pragma unroll 1
             for (int j = 0; j < nk; ++j) {
                 const int64_t lo = (int64_t)(k0 + j) * a.lstride;
                 const T* U = a.u + lo;

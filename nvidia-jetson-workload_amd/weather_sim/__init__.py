@@ -13,6 +13,8 @@ from .weather_simulation import (  # noqa: F401
     SlabGroup,
     MultiGPUSimulation,
     SlabbedGrid,
+    SlabSimulation,
+    new_comm_id,
     RandomInitialCondition, SimulationConfig, SimulationModel, UniformInitialCondition, VortexInitialCondition,
     WeatherGrid, WeatherSimulation, WeatherSimulationWrapper, ZonalFlowInitialCondition, create_initial_condition,
     get_available_initial_conditions, get_device_info, is_cuda_available, register_all_initial_conditions)

@@ -853,6 +853,30 @@ class SlabGroup:
             s.get_current_grid()._set(name, a[..., s.row0:s.row0 + s.rows, :])
 
 
+def new_comm_id() -> bytes:
+    """Extension: a fresh RCCL communicator id (ws_hip.h ws_comm_get_unique_id, 128 bytes) for a
+    decomposition over processes: create it on ONE rank and hand the same bytes to every rank
+    (any channel: torch.distributed, MPI, a file), then build each rank's SlabSimulation."""
+    buf = (ctypes.c_uint8 * _native.COMM_ID_BYTES)()
+    check(lib.ws_comm_get_unique_id(buf))
+    return bytes(buf)
+
+
+class SlabSimulation(WeatherSimulation):
+    """Extension: rank `rank` of `nranks` processes, one GPU each
+    (config.device_id), owning rows [row0, row0 + rows) of the global grid config describes;
+    halo rows move over RCCL inside run() (ws_hip.h ws_sim_create_slab). Every collective call
+    (run, step, run_until, get_cfl, initialize's IC) must be made by every rank alike. Fields
+    read or written through its grid are its own rows; results equal one domain bit for bit.
+    (One process driving several GPUs: MultiGPUSimulation / config.devices.)"""
+
+    def __init__(self, config: SimulationConfig, rank: int, nranks: int, comm_id: bytes):
+        if comm_id is None or len(comm_id) != _native.COMM_ID_BYTES:
+            raise ValueError(f"comm_id must be the {_native.COMM_ID_BYTES} bytes of new_comm_id() from one rank")
+        super().__init__(config, _slab=(int(rank), int(nranks), bytes(comm_id)))
+        self.rank, self.nranks = int(rank), int(nranks)
+
+
 class SlabbedGrid(WeatherGrid):
     """Extension: the global view of one grid slot of a y-slab decomposition (a
     MultiGPUSimulation's current grid). Field reads assemble the (H, W) / (L, H, W) array

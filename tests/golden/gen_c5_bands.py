@@ -17,7 +17,13 @@ tests/test_gpu_c5.py).
 Bands: the global top, the seam between slabs 0 and 1 of an 8-way split (row 2048), the
 middle (seam of slabs 3 / 4, row 8192), the global bottom. ICs: jet_stream (the bench
 workload) and random (seed 42: every cell differs, so x- and y-tiling seams are all live).
+
+  python gen_c5_bands.py             -> ref_c5_bands.json   (4 steps, the four bands above)
+  python gen_c5_bands.py --steps 50  -> ref_c5_bands50.json (C5's benchmark length, SURVEY
+                                        §8(d): 200-row cone margins, a band at EVERY seam of
+                                        the 8-way split, 2048 k +- 32 rows, k = 1..7)
 """
+import argparse
 import hashlib
 import json
 import os
@@ -32,12 +38,18 @@ sys.path.insert(0, HERE)
 from gen_golden import REF, read_snap, run_spec  # noqa: E402
 
 W = H = 16384
-STEPS = 4
-MARGIN = 4 * STEPS   # RK4: 4 rows of cone per step
 K = 64               # compared rows per band
-# compared rows [y0, y0 + K) per band
-BANDS = {"top": 0, "seam2048": 2048 - K // 2, "mid8192": 8192 - K // 2, "bottom": H - K}
 ICS = {"jet_stream": [], "random": ["42", "1.0"]}
+
+
+def bands(steps):
+    """Compared rows [y0, y0 + K) per band."""
+    if steps == 4:
+        return {"top": 0, "seam2048": 2048 - K // 2, "mid8192": 8192 - K // 2, "bottom": H - K}
+    out = {"top": 0}
+    out.update({f"seam{2048 * k}": 2048 * k - K // 2 for k in range(1, 8)})
+    out["bottom"] = H - K
+    return out
 
 
 def digest(a):
@@ -45,6 +57,13 @@ def digest(a):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=4)
+    args = ap.parse_args()
+    STEPS = args.steps
+    MARGIN = 4 * STEPS   # RK4: 4 rows of cone per step
+    BANDS = bands(STEPS)
+    name_out = "ref_c5_bands.json" if STEPS == 4 else f"ref_c5_bands{STEPS}.json"
     out = {"width": W, "height": H, "steps": STEPS, "method": 2, "variant": "f64", "compared_rows": K, "cases": {}}
     with tempfile.TemporaryDirectory(prefix="ws_c5_", dir="/tmp") as tmp:
         for ic, params in ICS.items():
@@ -75,7 +94,7 @@ def main():
                     case["l2"][f] = float(np.linalg.norm(a.astype(np.float64)))
                 out["cases"][f"{ic}/{name}"] = case
                 print(ic, name, case["rows"], case["l2"], flush=True)
-    with open(os.path.join(HERE, "ref_c5_bands.json"), "w") as f:
+    with open(os.path.join(HERE, name_out), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
 

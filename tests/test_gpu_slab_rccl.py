@@ -51,6 +51,23 @@ def test_one_rank_rccl_slab_matches_single_domain(method, fp64):
     slab.comm_barrier()
 
 
+def test_public_slab_simulation_api():
+    """The public form of a rank (weather_sim.SlabSimulation + new_comm_id; no bench.py
+    helpers, no private kwargs): one rank of one, equal to one domain."""
+    c = ws.SimulationConfig()
+    c.grid_width, c.grid_height, c.integration_method = 128, 40, 2
+    one = ws.WeatherSimulation(c)
+    slab = ws.SlabSimulation(c, 0, 1, ws.new_comm_id())
+    assert (slab.rank, slab.nranks, slab.row0, slab.rows) == (0, 1, 0, 40)
+    for s in (one, slab):
+        s.set_initial_condition(ws.JetStreamInitialCondition())
+        s.initialize()
+        assert s.run(6) == 6
+    np.testing.assert_array_equal(slab.get_current_grid().get_height_field(), one.get_current_grid().get_height_field())
+    with pytest.raises(ValueError):
+        ws.SlabSimulation(c, 0, 1, b"short")
+
+
 @pytest.mark.parametrize("block", ["1", "2", "3"])
 @pytest.mark.parametrize("kernel", ["dppy", "x2y", "lds"])
 @pytest.mark.parametrize("method", [0, 1, 2])

@@ -52,27 +52,29 @@ if __name__ == "__main__":
 #
 # The bvort RK4 fp64 fault of rounds 2-3: the compiler lowered a switch over
 # stores with the store pointer as a phi whose SGPR pair was `implicit-def` (undefined) on one
-# edge, and the store's 64-bit VGPR address was then computed from that pair. No source-level
-# index was out of range. This rule finds the pattern in DISASSEMBLED code (the built library's
-# gfx950 code objects, where no implicit-def comments survive) by a forward may-be-undefined
-# analysis over each kernel's control-flow graph:
-#   * at entry every SGPR beyond the hardware-preloaded ones (user SGPRs, workgroup ids /
-#     info, private segment offset: the kernel descriptor's COMPUTE_PGM_RSRC2) is undefined;
-#     VGPRs are taken as defined (undefinedness is only tracked from SGPRs: VGPR merges of
-#     exec-masked branches would otherwise flag every structurized if / else);
-#   * an instruction's destinations become undefined iff one of its register sources is;
-#   * at a join, a register is undefined if it is on ANY incoming path;
-#   * a global / buffer / flat store whose address operands (vaddr, saddr, srsrc, soffset)
-#     may be undefined is reported.
+# edge; the store's 64-bit VGPR address was then computed from that pair, and the store wrote
+# through whatever the SGPRs still held. No source-level index was out of range, and in the
+# code object nothing shows it (the SGPRs hold a stale, valid-looking value). The compiler's
+# assembly keeps the fact as `; implicit-def: $sgpr8_sgpr9` comments, so the rule runs on the
+# gfx950 assembly the library was built from (the Makefile keeps it: -save-temps=obj, which
+# leaves the instruction stream bit-identical), by a forward may-be-undefined analysis over
+# each kernel's control-flow graph:
+#   * an SGPR implicit-def makes its registers undefined from that point (SGPRs are
+#     wave-uniform: the undefined edge is a path the whole wave takes; VGPR implicit-defs are
+#     the exec-masked arms of divergent if / else and are not followed);
+#   * an instruction's destinations become undefined iff one of its register sources is
+#     (and defined again when all its sources are defined);
+#   * at a join a register is undefined if it is on ANY incoming path;
+#   * a global / buffer / flat store (or atomic) whose address operands (vaddr, saddr,
+#     srsrc, soffset) may be undefined is reported.
 # ---------------------------------------------------------------------------------------
-import struct
-
-_REG = re.compile(r"^(?:(?P<k>[sv])(?P<n>\d+)|(?P<kk>[sv])\[(?P<a>\d+):(?P<b>\d+)\]|(?P<sp>vcc|vcc_lo|vcc_hi|m0))$")
+_REG = re.compile(r"^(?:(?P<k>[sv])(?P<n>\d+)|(?P<kk>[sv])\[(?P<a>\d+):(?P<b>\d+)\]|(?P<sp>vcc|vcc_lo|vcc_hi))$")
 _NO_DEST = re.compile(r"^(s_cmp|s_bitcmp|s_cbranch|s_branch|s_waitcnt|s_nop|s_endpgm|s_barrier|s_setprio|s_sleep|"
                       r"s_sendmsg|s_setreg|s_set_gpr_idx|s_trap|s_icache|s_dcache|s_ttrace|s_wait|s_delay|s_sethalt|"
-                      r"s_setkill|s_cbranch|s_code_end|s_incperflevel|s_decperflevel|"
-                      r"buffer_store|global_store|flat_store|scratch_store|ds_write|ds_store|exp|"
+                      r"s_setkill|s_code_end|s_incperflevel|s_decperflevel|s_sched|"
+                      r"buffer_store|global_store|flat_store|scratch_store|ds_write|ds_store|exp\b|"
                       r"buffer_wbl2|buffer_inv|buffer_wbinvl1|s_store|s_scratch_store|s_buffer_store)")
+_MIR = re.compile(r"\$(sgpr|vgpr)(\d+)")
 
 
 def _regset(tok):
@@ -91,11 +93,14 @@ def _regset(tok):
     return {"vcc"}
 
 
-def _dests_and_srcs(ins):
+def _operands(rest):
+    return [o.strip().split()[0] for o in rest.split(",") if o.strip()]
+
+
+def dests_and_srcs(ins):
     """(destination registers, source registers) of one instruction (text)."""
     op, _, rest = ins.partition(" ")
-    ops = [o for o in (x.strip() for x in rest.split(",")) if o]
-    toks = [o.split()[0] if o.split() else o for o in ops]  # drop modifiers glued after a space
+    toks = _operands(rest)
     regs = [_regset(t) for t in toks]
     if not regs or _NO_DEST.match(op):
         return set(), set().union(*regs) if regs else set()
@@ -107,19 +112,20 @@ def _dests_and_srcs(ins):
     if re.match(r"v_(add|sub|subrev)(_co|c_co|b_co)?_u32|v_addc|v_subb|v_div_scale|v_mad_[iu]64", op) and len(regs) > 2 \
             and (toks[1].startswith("s") or toks[1].startswith("vcc")):
         dests |= regs[1]
-        srcs = set().union(*regs[2:]) if len(regs) > 2 else set()
+        srcs = set().union(*regs[2:])
     return dests, srcs
 
 
-def _store_addr_regs(ins):
+def store_addr_regs(ins):
+    """Address registers of a global / buffer / flat store or atomic; None for other ops."""
     op, _, rest = ins.partition(" ")
-    toks = [o.strip().split()[0] for o in rest.split(",") if o.strip()]
-    if op.startswith("global_store") or op.startswith("global_atomic") or op.startswith("flat_store"):
+    toks = _operands(rest)
+    if op.startswith(("global_store", "global_atomic", "flat_store", "flat_atomic")):
         regs = set(_regset(toks[0])) if toks else set()
         if len(toks) > 2:
             regs |= _regset(toks[2])  # saddr (or 'off')
         return regs
-    if op.startswith("buffer_store") or op.startswith("buffer_atomic"):
+    if op.startswith(("buffer_store", "buffer_atomic")):
         regs = set()
         for t in toks[1:4]:  # vaddr (or off), srsrc, soffset
             regs |= _regset(t)
@@ -127,132 +133,195 @@ def _store_addr_regs(ins):
     return None
 
 
-_LINE = re.compile(r"^\s+(?P<ins>[a-z_][^/]*?)\s*//\s*(?P<addr>[0-9A-Fa-f]+):[^<]*(?:<(?P<tgt>[^>+]+)(?:\+0x(?P<off>[0-9a-fA-F]+))?>)?\s*$")
-_FUNC = re.compile(r"^(?P<addr>[0-9a-fA-F]+) <(?P<name>[^>]+)>:$")
-
-
-def parse_functions(lines):
-    """{name: (start address, [(address, instruction, branch target address or None)])} from
-    llvm-objdump -d output."""
-    funcs, cur = {}, None
+def parse_asm_kernels(lines):
+    """{kernel: [item]} from compiler (-S) assembly; an item is ("label", name),
+    ("undef", regs) for an implicit-def comment, or ("ins", text)."""
+    kernels, cur = {}, None
+    globl = set()
     for l in lines:
-        m = _FUNC.match(l)
+        st = l.strip()
+        m = re.match(r"^\.globl\s+(\S+)", st)
         if m:
-            cur = m.group("name")
-            funcs[cur] = (int(m.group("addr"), 16), [])
+            globl.add(m.group(1))
             continue
-        m = _LINE.match(l)
-        if m and cur is not None:
-            tgt = None
-            if m.group("tgt") and m.group("ins").startswith(("s_branch", "s_cbranch")):
-                base = funcs.get(m.group("tgt"), (None,))[0]
-                if base is not None:
-                    tgt = base + int(m.group("off") or "0", 16)
-            funcs[cur][1].append((int(m.group("addr"), 16), m.group("ins").strip(), tgt))
-    return funcs
+        m = re.match(r"^([A-Za-z_.$][\w.$]*):", l)
+        if m and not l.startswith("\t") and not l.startswith(" "):
+            name = m.group(1)
+            if name in globl and not name.startswith("."):
+                cur = name
+                kernels[cur] = []
+                continue
+            if cur is not None and name.startswith(".LBB"):
+                kernels[cur].append(("label", name))
+            continue
+        if cur is None:
+            continue
+        if st.startswith("; %bb."):
+            kernels[cur].append(("label", st[2:].split()[0]))  # fallthrough block
+            continue
+        if st.startswith("; implicit-def:"):
+            # SGPRs only: an SGPR is wave-uniform, so "undefined on an edge" is a real path of
+            # the whole wave (the round-3 store pointer). VGPR implicit-defs mark the two arms
+            # of a divergent if / else writing one value (e.g. the 64-bit division expansion):
+            # the exec-masked, structurized CFG has "neither arm" paths that no lane takes.
+            regs = {"s" + n for k, n in _MIR.findall(st) if k == "sgpr"}
+            if regs:
+                kernels[cur].append(("undef", regs))
+            continue
+        if st.startswith(".Lfunc_end") or st.startswith(".size") or st.startswith("s_endpgm") and False:
+            continue
+        t = st.split(";")[0].strip()
+        if not t or t.startswith(".") or t.endswith(":"):
+            continue
+        kernels[cur].append(("ins", t))
+    return kernels
 
 
-def undefined_address_stores(ins_list, npreload):
-    """Stores of one kernel whose address may be undefined: [(address, instruction, regs)]."""
-    if not ins_list:
+_IMM = re.compile(r"^-?(0x[0-9a-fA-F]+|\d+)$")
+
+
+def _imm(tok):
+    return int(tok, 0) if _IMM.match(tok) else None
+
+
+def undefined_address_stores(items, max_contexts=8):
+    """Stores of one kernel whose address may be undefined: [(item index, store, regs)].
+
+    Path-sensitive in the one way the compiler's lowering needs: SGPRs set to constants
+    (s_mov_b32 / s_mov_b64 of an immediate) are tracked per path, and a branch on vcc derived
+    from such a constant mask (s_and[n2]_b64 vcc, exec, s[..]) follows only its feasible edge
+    (exec assumed non-zero). That is how the compiler guards "defined on the other path":
+    e.g. `s_mov_b64 s[2:3], -1; implicit-def s27; ... s_andn2_b64 vcc, exec, s[2:3];
+    s_cbranch_vccnz` never reaches the use with s27 undefined. Up to max_contexts constant
+    environments per block; beyond that they merge (constants that differ are dropped)."""
+    blocks, labels, cur = [], {}, []
+    for i, it in enumerate(items):
+        if it[0] == "label":
+            if cur:
+                blocks.append(cur)
+            cur = []
+            labels[it[1]] = len(blocks)
+            continue
+        cur.append(i)
+        if it[0] == "ins" and it[1].startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc")):
+            blocks.append(cur)
+            cur = []
+    if cur:
+        blocks.append(cur)
+    if not blocks:
         return []
-    addrs = [a for a, _, _ in ins_list]
-    index = {a: i for i, a in enumerate(addrs)}
-    leaders = {0}
-    for i, (a, t, tgt) in enumerate(ins_list):
-        if t.startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc", "s_swappc")):
-            if i + 1 < len(ins_list):
-                leaders.add(i + 1)
-            if tgt is not None and tgt in index:
-                leaders.add(index[tgt])
-    starts = sorted(leaders)
-    blocks = [(s, (starts[k + 1] if k + 1 < len(starts) else len(ins_list))) for k, s in enumerate(starts)]
-    bid = {s: k for k, (s, _) in enumerate(blocks)}
-    succ = []
-    for s, e in blocks:
-        a, t, tgt = ins_list[e - 1]
+
+    def step(taint, const, vcc, it):
+        """Transfer one item; vcc: None unknown, 0 zero, 1 non-zero."""
+        if it[0] == "undef":
+            taint = taint | it[1]
+            const = {k: v for k, v in const.items() if k not in it[1]}
+            return taint, const, vcc
+        if it[0] != "ins":
+            return taint, const, vcc
+        t = it[1]
+        op, _, rest = t.partition(" ")
+        toks = _operands(rest)
+        d, src = dests_and_srcs(t)
+        if d:
+            taint = (taint | d) if (src & taint) else (taint - d)
+            const = {k: v for k, v in const.items() if k not in d}
+            if op in ("s_mov_b32", "s_mov_b64") and len(toks) == 2 and _imm(toks[1]) is not None:
+                for r in d:
+                    const[r] = _imm(toks[1])
+            if "vcc" in d:
+                vcc = None
+                if op in ("s_and_b64", "s_andn2_b64") and len(toks) == 3 and toks[1] == "exec":
+                    regs = sorted(_regset(toks[2]))
+                    vals = [const.get(r) for r in regs]
+                    if regs and all(v is not None for v in vals):
+                        allone = all(v in (-1, 0xffffffff) for v in vals)
+                        zero = all(v == 0 for v in vals)
+                        if op == "s_and_b64":
+                            vcc = 0 if zero else 1 if allone else None
+                        else:
+                            vcc = 0 if allone else 1 if zero else None
+        return taint, const, vcc
+
+    def successors(b, vcc):
+        idx = blocks[b]
+        last = items[idx[-1]] if idx else ("", "")
         out = []
-        if tgt is not None and tgt in index:
-            out.append(bid[index[tgt]])
-        if not t.startswith(("s_branch", "s_endpgm", "s_setpc")) and e < len(ins_list):
-            out.append(bid[e])
-        succ.append(out)
-    undef0 = {f"s{k}" for k in range(npreload, 106)} | {"vcc"}
-    IN = [None] * len(blocks)
-    IN[0] = set(undef0)
-    work = [0]
-    OUT = [None] * len(blocks)
+        fall = b + 1 < len(blocks)
+        if last[0] == "ins":
+            op, _, rest = last[1].partition(" ")
+            tgt = labels.get(rest.strip())
+            if op.startswith("s_branch"):
+                return [tgt] if tgt is not None else []
+            if op.startswith(("s_endpgm", "s_setpc")):
+                return []
+            if op.startswith("s_cbranch") and tgt is not None:
+                taken = fall_ok = True
+                if op == "s_cbranch_vccnz" and vcc is not None:
+                    taken, fall_ok = vcc == 1, vcc == 0
+                elif op == "s_cbranch_vccz" and vcc is not None:
+                    taken, fall_ok = vcc == 0, vcc == 1
+                if taken:
+                    out.append(tgt)
+                if fall and fall_ok:
+                    out.append(b + 1)
+                return out
+        return [b + 1] if fall else []
+
+    # contexts per block: {frozenset(const items): taint}
+    IN = [dict() for _ in blocks]
+    IN[0][frozenset()] = frozenset()
+    work = [(0, frozenset())]
     while work:
-        b = work.pop()
-        st = set(IN[b])
-        s, e = blocks[b]
-        for _, t, _ in ins_list[s:e]:
-            d, src = _dests_and_srcs(t)
-            if d:
-                if src & st:
-                    st |= d
-                else:
-                    st -= d
-        OUT[b] = st
-        for n in succ[b]:
-            new = st if IN[n] is None else (IN[n] | st)
-            if IN[n] is None or new != IN[n]:
-                IN[n] = new
-                work.append(n)
-    hits = []
-    for b, (s, e) in enumerate(blocks):
-        if IN[b] is None:
-            continue  # unreachable
-        st = set(IN[b])
-        for a, t, _ in ins_list[s:e]:
-            regs = _store_addr_regs(t)
-            if regs is not None and regs & st:
-                hits.append((a, t, sorted(regs & st)))
-            d, src = _dests_and_srcs(t)
-            if d:
-                if src & st:
-                    st |= d
-                else:
-                    st -= d
+        b, key = work.pop()
+        if key not in IN[b]:
+            continue  # a context since merged into another (its work item is queued)
+        taint, const, vcc = set(IN[b][key]), dict(key), None
+        for i in blocks[b]:
+            taint, const, vcc = step(taint, const, vcc, items[i])
+        for n in successors(b, vcc):
+            k2 = frozenset(const.items())
+            ctx = IN[n]
+            if k2 not in ctx and len(ctx) >= max_contexts:
+                # merge everything into one context: keep only constants all contexts agree on
+                common = None
+                tall = set(taint)
+                for kk, tt in ctx.items():
+                    common = set(kk) if common is None else common & set(kk)
+                    tall |= tt
+                common = (common or set()) & set(k2)
+                ctx.clear()
+                ctx[frozenset(common)] = frozenset(tall)
+                work.append((n, frozenset(common)))
+                continue
+            if k2 in ctx:
+                merged = ctx[k2] | frozenset(taint)
+                if merged == ctx[k2]:
+                    continue
+                ctx[k2] = merged
+            else:
+                # a key may have been collapsed by a merge: fold into the surviving context
+                ctx[k2] = frozenset(taint)
+            work.append((n, k2))
+    hits, seen = [], set()
+    for b, idx in enumerate(blocks):
+        for key, t0 in IN[b].items():
+            taint, const, vcc = set(t0), dict(key), None
+            for i in idx:
+                it = items[i]
+                if it[0] == "ins" and i not in seen:
+                    regs = store_addr_regs(it[1])
+                    if regs is not None and regs & taint:
+                        hits.append((i, it[1], sorted(regs & taint)))
+                        seen.add(i)
+                taint, const, vcc = step(taint, const, vcc, it)
     return hits
 
 
-def kernel_preloads(path):
-    """{kernel name: SGPRs the hardware preloads} from the kernel descriptors (<name>.kd
-    symbols) of a gfx950 code object: user SGPRs + workgroup id x / y / z + workgroup info +
-    private segment wave offset (COMPUTE_PGM_RSRC2, the AMDHSA kernel descriptor at +52)."""
-    data = open(path, "rb").read()
-    shoff, = struct.unpack_from("<Q", data, 0x28)
-    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
-    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
-    out = {}
-    for sec in secs:
-        if sec[1] != 2:  # SHT_SYMTAB
-            continue
-        strtab = secs[sec[6]]
-        for k in range(sec[5] // 24):
-            name_off, info, other, shndx, value, size = struct.unpack_from("<IBBHQQ", data, sec[4] + k * 24)
-            end = data.index(b"\0", strtab[4] + name_off)
-            name = data[strtab[4] + name_off:end].decode()
-            if not name.endswith(".kd") or shndx == 0 or shndx >= len(secs):
-                continue
-            tsec = secs[shndx]
-            rsrc2, = struct.unpack_from("<I", data, tsec[4] + (value - tsec[3]) + 52)
-            n = ((rsrc2 >> 1) & 31) + sum((rsrc2 >> b) & 1 for b in (7, 8, 9, 10)) + (rsrc2 & 1)
-            out[name[:-3]] = n
-    return out
-
-
-def scan_code_object(path, objdump):
-    """Rule 2 over one gfx950 code object: [(kernel, address, store, undefined regs)], and the
-    number of stores examined."""
-    import subprocess
-    pre = kernel_preloads(path)
-    dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", path], capture_output=True, text=True, check=True).stdout
+def scan_asm(lines):
+    """Rule 2 over compiler assembly: ([(kernel, store, undefined regs)], stores examined)."""
     hits, stores = [], 0
-    for name, (_, ins) in parse_functions(dis.splitlines()).items():
-        if name not in pre:
-            continue  # not a kernel entry
-        stores += sum(_store_addr_regs(t) is not None for _, t, _ in ins)
-        hits += [(name, a, t, r) for a, t, r in undefined_address_stores(ins, pre[name])]
+    for name, items in parse_asm_kernels(lines).items():
+        stores += sum(1 for it in items if it[0] == "ins" and store_addr_regs(it[1]) is not None)
+        hits += [(name, t, r) for _, t, r in undefined_address_stores(items)]
     return hits, stores
