@@ -132,7 +132,7 @@ int32_t ws_sim::seg_rows(int nst) const {
 namespace wsr {
 
 void sim_free(ws_sim* s) {
-    for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3})
+    for (ws_grid* g : {s->slot[0], s->slot[1], s->tmpA, s->tmpB, s->K2, s->K3, s->ov[0], s->ov[1], s->ov[2], s->ov[3]})
         if (g) { grid_free(g); delete g; }
     for (hipEvent_t e : {s->ev0, s->ev1, s->aux_in, s->aux_out, s->ev_edge, s->ev_join, s->ev_trial[0], s->ev_trial[1]})
         if (e) (void)hipEventDestroy(e);

@@ -6,8 +6,8 @@
 //   * one domain: one fused launch per one or two time steps (temporal blocking), or the
 //     per-stage kernels (WS_FUSED=0);
 //   * a y-slab of a multi-GPU decomposition: deep-halo blocks of up to 6 steps per halo
-//     exchange, stream-ordered or overlapped (each block's last and first launches split by
-//     rows so the exchange runs on a second stream beside their interiors, overlap_launch);
+//     exchange, stream-ordered or overlapped (the exchange behind the edge bands on a second
+//     stream while the interior runs, overlap_block);
 // then the reference's grid rotation, the PE T / P update and the float time accumulation.
 #include <algorithm>
 #include <cstdio>
@@ -450,117 +450,138 @@ static void enqueue_steps(ws_sim* s, int nsteps) {
 
 // ------------------------------------------------------------------------------------
 // Slab overlap schedule (north_star: the halo exchange overlapped with interior compute on a
-// second HIP stream), round 5: split launches. The stream-ordered schedule runs a block as
-// exchange(k) -> L_0 -> L_1 -> ... -> L_last with the exchange alone on the compute stream.
-// Here the exchange of block k leaves the critical path:
-//   * block k-1's LAST launch is split by rows: A = the rows the neighbours need next,
-//     [0, D) and [H - D, H), first, on the slab's `edge` stream (behind the launches before
-//     it), and B = the rest, [D, H - D), on the compute stream; the exchange of block k's halo
-//     follows A on the edge stream;
-//   * block k's FIRST launch is split too: C = the rows whose cone stays inside the owned rows,
-//     [cone, H - cone), on the compute stream (after A and B), and E = the rows that read the
-//     halo, [-e, cone) and [H - cone, H + e), on the edge stream behind the exchange (and B);
-//   * the block's next launch waits for E.
-// The exchange so runs beside B and C, two nearly full launches, for two thin launches (A, E)
-// per block. (Rounds 2-4 advanced 2D-row edge bands through the whole block in grids of their
-// own: three latency-bound edge launches per block on the critical path, which lost to the
-// stream-ordered schedule at 8 ranks.) Every row of every launch is computed once, from the same
-// inputs as in the stream-ordered schedule: bit-identical. A block of one launch, or a slab too
-// thin for B and C, runs stream-ordered.
+// second HIP stream). A block of `steps` steps (one halo exchange, depth D = steps x NST
+// rows, as in the stream-ordered schedule above) is split by rows:
+//   * edge bands, on the slab's `edge` stream: the rows within 2D of a non-global side,
+//     advanced the whole block through their own ping-pong grids (ov[2], ov[3]); launch j
+//     (cumulative cone C_j) computes rows [C_j - D, 2D - C_j) at the top and
+//     [H - 2D + C_j, H + D - C_j) at the bottom, so the last launch writes exactly rows
+//     [0, D) and [H - D, H) of the next grid -- the rows the neighbours need. The exchange of
+//     the next block's halo follows on the same stream;
+//   * interior, on the compute stream meanwhile: launch j computes rows [C_j, H - C_j)
+//     through ov[0], ov[1]; it reads only owned rows (never the halo), and its last launch
+//     writes rows [D, H - D) of the next grid.
+// Every launch reads exactly the rows its predecessor in the same band wrote (the
+// dependency cone shrinks by the launch's NST x steps per side), so both parts are
+// bit-identical to the stream-ordered schedule. Two cross-stream waits per block: the edge
+// launches of block k read rows [D, 2D) that the interior of block k-1 wrote (ev_join), and
+// the interior of block k reads rows [0, D) that the edges of block k-1 wrote (ev_edge). The
+// exchange itself is waited on only by the next block's edges (stream order on `edge`).
 // ------------------------------------------------------------------------------------
 
-// the edge stream and its events (created on first use)
-void ensure_overlap_streams(ws_sim* s) {
-    if (s->edge) return;
-    // (a high-priority edge stream measured no different in round 2: tools/rank_timing.py)
-    WS_HIP_CHECK(hipStreamCreateWithFlags(&s->edge, hipStreamNonBlocking));
-    WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
-    WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+// steps per launch within a block (2 while the tuned configuration launches two at once)
+static std::vector<int> block_launches(const ws_sim* s, int steps) {
+    std::vector<int> n;
+    for (int left = steps; left > 0;) {
+        const int k = launch_of(s, left);
+        n.push_back(k);
+        left -= k;
+    }
+    return n;
 }
 
-// Which split (if any) the next launch of `nsteps` steps takes. more: another launch follows
-// in this run segment.
-OverlapSplit overlap_split(const ws_sim* s, int nsteps, bool more) {
-    const int nst = fused_stages(s), cone = nsteps * nst, D = s->block * nst, H = s->slot[0]->H;
-    const bool first = s->block_pos == 0, last = s->block_pos + nsteps == s->block;
-    if (first && s->halo_inflight) return OverlapSplit::kFirst;  // C / E (the exchange is in flight)
-    if (last && !first && more && H > 2 * D && H > 2 * cone) return OverlapSplit::kLast;  // A / B
-    return OverlapSplit::kNone;
+// launch j's interior rows and edge-band rows (two ranges; merged into A when they touch)
+struct BandRows {
+    RowRange interior, A, B;
+};
+
+static BandRows band_rows(const ws_grid* g, int C, int D) {
+    const int H = g->H;
+    const int lo = g->top_clamp ? 0 : C - D, hi = g->bot_clamp ? H : H + D - C;
+    BandRows r{{g->top_clamp ? 0 : C, g->bot_clamp ? H : H - C}, {0, 0}, {0, 0}};
+    RowRange top{0, 0}, bot{0, 0};
+    if (!g->top_clamp) top = {lo, std::min(hi, 2 * D - C)};
+    if (!g->bot_clamp) bot = {std::max(lo, H - 2 * D + C), hi};
+    if (top.rows() > 0 && bot.rows() > 0 && top.y1 >= bot.y0) {
+        r.A = {top.y0, bot.y1};
+    } else {
+        r.A = top.rows() > 0 ? top : bot;
+        r.B = top.rows() > 0 ? bot : RowRange{0, 0};
+    }
+    return r;
 }
 
-// kLast, part 1 (edge stream): A, the rows the neighbours need; ev_edge marks it done. The
-// exchange follows on the edge stream (the caller's: RCCL, or the slab group's copies).
-template <typename T>
-void overlap_launch_a(ws_sim* s, int nsteps) {
-    const int nst = fused_stages(s), D = s->block * nst;
-    const ws_grid* c = s->slot[s->cur];
-    WS_HIP_CHECK(hipEventRecord(s->ev_join, s->stream));  // the launches before
+// the overlap grids (allocated on first use; same layout and slab flags as the slots)
+void ensure_overlap_grids(ws_sim* s) {
+    if (!s->edge) {
+        // (a high-priority edge stream measured no different: tools/rank_timing.py)
+        WS_HIP_CHECK(hipStreamCreateWithFlags(&s->edge, hipStreamNonBlocking));
+        WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
+        WS_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    }
+    const ws_grid* c = s->slot[0];
+    for (auto& g : s->ov) {
+        if (g) continue;
+        g = new_grid(c->W, c->H, c->L, s->dtype, s->device, 3, s->stream);
+        g->owned = true;
+        g->dx = c->dx; g->dy = c->dy;
+        g->top_clamp = c->top_clamp; g->bot_clamp = c->bot_clamp;
+        g->row0 = c->row0; g->gH = c->gH;
+    }
+}
+
+// Phase 1 (compute stream): join the previous block and hand the edge stream its start.
+void overlap_begin(ws_sim* s, bool first) {
+    if (!first) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // rows [0, D) of block k-1
+    WS_HIP_CHECK(hipEventRecord(s->ev_join, s->stream));
     WS_HIP_CHECK(hipStreamWaitEvent(s->edge, s->ev_join, 0));
-    fused_launch<T>(s, nst, nsteps, c->top_clamp ? RowRange{0, 0} : RowRange{0, D},
-                    c->bot_clamp ? RowRange{0, 0} : RowRange{c->H - D, c->H}, s->seg_rows(nst), s->edge);
+}
+
+// Phase 2 (edge stream): the edge bands of the block; ev_edge marks them done.
+template <typename T>
+void overlap_edges(ws_sim* s, int steps) {
+    const int nst = fused_stages(s), D = steps * nst;
+    const std::vector<int> n = block_launches(s, steps);
+    ws_grid* in = s->slot[s->cur];
+    int C = 0;
+    for (size_t j = 0; j < n.size(); ++j) {
+        C += n[j] * nst;
+        ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[2 + j % 2];
+        const BandRows r = band_rows(in, C, D);
+        // the tuned segment rows (one segment per band -- fewer warm-up rows, longer marches
+        // -- measured no faster: the edges are on the critical path at 8 slabs)
+        fused_launch<T>(s, nst, n[j], r.A, r.B, s->seg_rows(nst), s->edge, in, out);
+        in = out;
+    }
     WS_HIP_CHECK(hipEventRecord(s->ev_edge, s->edge));
 }
 
-// kLast, part 2 (compute stream): B, the other rows; the next block's halo is now in flight.
+// Phase 3 (compute stream): the interior of the block, then the PE T / P update and rotation.
 template <typename T>
-void overlap_launch_b(ws_sim* s, int nsteps) {
-    const int nst = fused_stages(s), D = s->block * nst;
-    const ws_grid* c = s->slot[s->cur];
-    const RowRange B{c->top_clamp ? 0 : D, c->bot_clamp ? c->H : c->H - D};
-    fused_launch<T>(s, nst, nsteps, B, {0, 0}, s->seg_rows(nst), s->stream);
-    s->halo_inflight = true;
-}
-
-// kFirst (the edge stream has the exchange queued): E on the edge stream after B, C on the
-// compute stream after A, and the compute stream waits for E before anything else.
-template <typename T>
-void overlap_launch_first(ws_sim* s, int nsteps) {
-    const int nst = fused_stages(s), cone = nsteps * nst;
-    const ws_grid* c = s->slot[s->cur];
-    const RowRange rows = step_rows(s, nst, nsteps);
-    WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // A (C reads its rows)
-    WS_HIP_CHECK(hipEventRecord(s->ev_join, s->stream));         // B (E may read its rows)
-    WS_HIP_CHECK(hipStreamWaitEvent(s->edge, s->ev_join, 0));
-    fused_launch<T>(s, nst, nsteps, c->top_clamp ? RowRange{0, 0} : RowRange{rows.y0, cone},
-                    c->bot_clamp ? RowRange{0, 0} : RowRange{c->H - cone, rows.y1}, s->seg_rows(nst), s->edge);
-    WS_HIP_CHECK(hipEventRecord(s->ev_edge, s->edge));
-    const RowRange C{c->top_clamp ? rows.y0 : cone, c->bot_clamp ? rows.y1 : c->H - cone};
-    fused_launch<T>(s, nst, nsteps, C, {0, 0}, s->seg_rows(nst), s->stream);
-    WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // E, before the next launch
-    s->halo_inflight = false;
+void overlap_interior(ws_sim* s, int steps) {
+    const int nst = fused_stages(s), D = steps * nst;
+    const std::vector<int> n = block_launches(s, steps);
+    ws_grid* in = s->slot[s->cur];
+    const ws::Geom g = in->geom();
+    int C = 0;
+    for (size_t j = 0; j < n.size(); ++j) {
+        C += n[j] * nst;
+        ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[j % 2];
+        const BandRows r = band_rows(in, C, D);
+        s->timer.begin(0, 6.0 * sizeof(T) * g.W * r.interior.rows() * g.L * n[j], s->stream);
+        fused_launch<T>(s, nst, n[j], r.interior, {0, 0}, s->seg_rows(nst), s->stream, in, out);
+        s->timer.end(s->stream);
+        in = out;
+    }
+    rotate<T>(s, steps);
 }
 
 // Whether run() uses the overlap schedule: a slab of the fused path whose grids all have the
-// configured spacing (the multi-step launches' later stages assume it).
-// (A one-rank RCCL slab runs it only when WS_SLAB_OVERLAP=1: no neighbours, no-op exchanges.)
+// configured spacing (the two-step launches' later stages assume it).
+// (A one-rank RCCL slab runs it only when WS_SLAB_OVERLAP=1: no edge bands, no-op exchanges.)
 bool overlap_active(const ws_sim* s) {
     return s->overlap && (s->nranks > 1 || s->comm) && use_fused(s) && config_spacing(s);
 }
 
-// One launch of a slab with an RCCL communicator (or the measurement slab) in the overlap
-// schedule, incl. its block's halo exchange and the rotation.
+// One overlapped block of a slab with an RCCL communicator.
 template <typename T>
-static void overlap_launch(ws_sim* s, int nsteps, bool more) {
-    const int nst = fused_stages(s), D = s->block * nst;
-    const OverlapSplit sp = overlap_split(s, nsteps, more);
-    if (sp != OverlapSplit::kNone) {  // (step_begin's timer start; step_end stops it)
-        const ws::Geom g = s->slot[0]->geom();
-        s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L * nsteps, s->stream);
-    }
-    switch (sp) {
-        case OverlapSplit::kFirst:
-            overlap_launch_first<T>(s, nsteps);
-            break;
-        case OverlapSplit::kLast:
-            overlap_launch_a<T>(s, nsteps);
-            slab_exchange(s, s->slot[1 - s->cur], 3, D, s->edge);  // the next block's halo, behind A
-            overlap_launch_b<T>(s, nsteps);
-            break;
-        default:
-            step_begin<T>(s, nsteps);  // (a block start exchanges on the compute stream)
-            break;
-    }
-    step_end<T>(s, nsteps);
+static void overlap_block(ws_sim* s, int steps, bool first, bool last) {
+    const int depth = s->block * fused_stages(s);
+    if (first) slab_exchange(s, s->slot[s->cur], 3, depth, s->stream);
+    overlap_begin(s, first);
+    overlap_edges<T>(s, steps);
+    if (!last) slab_exchange(s, s->slot[1 - s->cur], 3, depth, s->edge);  // the next block's halo, behind the edge bands
+    overlap_interior<T>(s, steps);
 }
 
 template <typename T>
@@ -644,14 +665,13 @@ void run_steps(ws_sim* s, int k) {
     // (marks: events recorded on the compute stream after the first block and after the last)
     auto segment = [&](int n_steps, bool ovl, hipEvent_t mark0 = nullptr, hipEvent_t mark1 = nullptr) {
         if (n_steps <= 0) return;
-        if (ovl) ensure_overlap_streams(s);
+        if (ovl) ensure_overlap_grids(s);
         s->block_pos = 0;
-        s->halo_inflight = false;
         for (int i = 0; i < n_steps;) {
-            const int n = launch_steps(s, n_steps - i);
+            const int n = ovl ? std::min(s->block, n_steps - i) : launch_steps(s, n_steps - i);
             if (ovl) {
-                if (s->dtype == WS_F64) overlap_launch<double>(s, n, i + n < n_steps);
-                else overlap_launch<float>(s, n, i + n < n_steps);
+                if (s->dtype == WS_F64) overlap_block<double>(s, n, i == 0, i + n == n_steps);
+                else overlap_block<float>(s, n, i == 0, i + n == n_steps);
             } else if (s->dtype == WS_F64) {
                 enqueue_steps<double>(s, n);
             } else {
@@ -670,6 +690,7 @@ void run_steps(ws_sim* s, int k) {
             if (mark0 && prev < s->block && i >= s->block) WS_HIP_CHECK(hipEventRecord(mark0, s->stream));
         }
         if (mark1) WS_HIP_CHECK(hipEventRecord(mark1, s->stream));
+        if (ovl) WS_HIP_CHECK(hipStreamWaitEvent(s->stream, s->ev_edge, 0));  // the last block's edge bands
     };
     // (the trial runs where the overlap schedule could: a fused slab with the configured spacing)
     const bool trial_ok = (s->nranks > 1 || s->comm) && use_fused(s) && config_spacing(s);
@@ -748,11 +769,9 @@ template void step_begin<float>(ws_sim*, int);
 template void step_begin<double>(ws_sim*, int);
 template void step_end<float>(ws_sim*, int);
 template void step_end<double>(ws_sim*, int);
-template void overlap_launch_a<float>(ws_sim*, int);
-template void overlap_launch_a<double>(ws_sim*, int);
-template void overlap_launch_b<float>(ws_sim*, int);
-template void overlap_launch_b<double>(ws_sim*, int);
-template void overlap_launch_first<float>(ws_sim*, int);
-template void overlap_launch_first<double>(ws_sim*, int);
+template void overlap_edges<float>(ws_sim*, int);
+template void overlap_edges<double>(ws_sim*, int);
+template void overlap_interior<float>(ws_sim*, int);
+template void overlap_interior<double>(ws_sim*, int);
 
 }  // namespace wsr

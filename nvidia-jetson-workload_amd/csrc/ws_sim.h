@@ -203,9 +203,8 @@ struct ws_sim {
     bool tune_free() const { return !kernel_env && !(kernel_fixed && seg_fixed && align_fixed && tb_fixed); }
     int32_t block = 1;        // slab: steps per halo exchange (deep halo), see step_rows
     int32_t block_pos = 0;    // position in the current block (0 = exchange first)
-    // slab overlap schedule (overlap_launch, ws_schedule.cpp): a block's last launch is split
-    // into A (edge stream; the neighbours' rows, then the exchange) and B (compute stream), the
-    // next block's first launch into E (edge stream, after the exchange) and C (compute stream)
+    // slab overlap schedule (overlap_block): a block's edge bands run on `edge`, the halo
+    // exchange follows them there, the interior runs meanwhile on `stream`
     int overlap_mode = wsr::kOverlapOff;  // off / on / auto (decided from a measured exchange)
     bool overlap = false;                 // the schedule in use
     double xfer_us = -1.0;                // measured halo exchange (auto mode), microseconds
@@ -214,7 +213,7 @@ struct ws_sim {
     hipEvent_t ev_trial[2] = {};
     hipStream_t edge = nullptr;
     hipEvent_t ev_edge = nullptr, ev_join = nullptr;
-    bool halo_inflight = false;  // the next block's halo exchange is queued on `edge` (after A)
+    ws_grid* ov[4] = {};      // interior ping-pong (0, 1), edge-band ping-pong (2, 3); u, v, h
     double emu_xfer_us = -1.0;  // measurement slab (ws_sim_create_slab_emulated): transfer stand-in
     // slab decomposition
     ws::SlabComm* comm = nullptr;
@@ -282,15 +281,12 @@ template <typename T>
 int fused_waves_per_simd(const ws_sim* s);  // occupancy of the chosen fused variant (0: none)
 // overlap schedule pieces (the slab group runs them per slab, ws_slab.cpp)
 bool overlap_active(const ws_sim* s);
-void ensure_overlap_streams(ws_sim* s);
-enum class OverlapSplit { kNone, kFirst, kLast };
-OverlapSplit overlap_split(const ws_sim* s, int nsteps, bool more);
+void ensure_overlap_grids(ws_sim* s);
+void overlap_begin(ws_sim* s, bool first);
 template <typename T>
-void overlap_launch_a(ws_sim* s, int nsteps);  // kLast: A on the edge stream
+void overlap_edges(ws_sim* s, int steps);
 template <typename T>
-void overlap_launch_b(ws_sim* s, int nsteps);  // kLast: B on the compute stream
-template <typename T>
-void overlap_launch_first(ws_sim* s, int nsteps);  // kFirst: E (edge) and C (compute)
+void overlap_interior(ws_sim* s, int steps);
 // the halo exchange of a slab (RCCL, or the measurement slab's stand-in)
 void slab_exchange(ws_sim* s, ws_grid* g, int nfields, int depth, hipStream_t st);
 double advance_time(const ws_sim* s, double t);  // t + dt in the simulation's precision

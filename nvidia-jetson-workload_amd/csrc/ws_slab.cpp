@@ -235,39 +235,26 @@ void group_exchange(ws_group* gr, int nfields, int depth, bool next = false, hip
                 WS_HIP_CHECK(ws::halo_unpack(plans[r], hf[r], side, gr->slabs[r]->staging->recv[side], st));
 }
 
-// One launch of every slab in the overlap schedule (overlap_launch, ws_schedule.cpp) with the
-// group's device-copy transport on xstream between the slabs' edge streams. Every slab takes
-// the same split (a slab too thin for it makes the whole group run the launch unsplit).
+// One overlapped block of every slab (overlap_block with the group's device-copy transport
+// on xstream between the slabs' edge streams).
 template <typename T>
-void group_overlap_launch(ws_group* gr, int nsteps, bool more) {
+void group_overlap_block(ws_group* gr, int steps, bool first, bool last) {
     ws_sim* s0 = gr->slabs[0];
     const int depth = s0->block * fused_stages(s0);
-    OverlapSplit sp = overlap_split(s0, nsteps, more);
-    for (ws_sim* s : gr->slabs)
-        if (overlap_split(s, nsteps, more) != sp) sp = OverlapSplit::kNone;
-    if (sp != OverlapSplit::kNone)
-        for (ws_sim* s : gr->slabs) {
-            const ws::Geom g = s->slot[0]->geom();
-            s->timer.begin(0, 6.0 * sizeof(T) * g.W * g.H * g.L * nsteps, s->stream);
-        }
-    if (sp == OverlapSplit::kFirst) {
-        for (ws_sim* s : gr->slabs) overlap_launch_first<T>(s, nsteps);
-    } else if (sp == OverlapSplit::kLast) {
-        for (ws_sim* s : gr->slabs) overlap_launch_a<T>(s, nsteps);
+    if (first) group_exchange(gr, 3, depth);
+    for (ws_sim* s : gr->slabs) overlap_begin(s, first);
+    for (ws_sim* s : gr->slabs) overlap_edges<T>(s, steps);
+    if (!last) {
         if (!gr->xstream) {
             WS_HIP_CHECK(hipStreamCreateWithFlags(&gr->xstream, hipStreamNonBlocking));
             WS_HIP_CHECK(hipEventCreateWithFlags(&gr->ev_x, hipEventDisableTiming));
         }
         for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(gr->xstream, s->ev_edge, 0));
-        group_exchange(gr, 3, depth, true, gr->xstream);  // the next block's halo, behind every A
+        group_exchange(gr, 3, depth, true, gr->xstream);
         WS_HIP_CHECK(hipEventRecord(gr->ev_x, gr->xstream));
         for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(s->edge, gr->ev_x, 0));
-        for (ws_sim* s : gr->slabs) overlap_launch_b<T>(s, nsteps);
-    } else {
-        if (s0->block_pos == 0) group_exchange(gr, 3, depth);  // a block start: its halo first
-        for (ws_sim* s : gr->slabs) step_begin<T>(s, nsteps);
     }
-    for (ws_sim* s : gr->slabs) step_end<T>(s, nsteps);
+    for (ws_sim* s : gr->slabs) overlap_interior<T>(s, steps);
 }
 
 // The auto schedule in a group: overlap where every slab has an interior (there is no
@@ -378,15 +365,13 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
         bool ovl = k > 0;  // every slab must agree
         for (ws_sim* s : gr->slabs) ovl = ovl && overlap_active(s);
         if (ovl)
-            for (ws_sim* s : gr->slabs) {
-                ensure_overlap_streams(s);
-                s->halo_inflight = false;
-            }
+            for (ws_sim* s : gr->slabs) ensure_overlap_grids(s);
         for (int i = 0; i < k;) {
             int n = 8;  // every slab must agree (they share the block position and the choice)
             for (ws_sim* s : gr->slabs) n = std::min(n, launch_steps(s, k - i));
-            if (ovl && s0->dtype == WS_F64) group_overlap_launch<double>(gr, n, i + n < k);
-            else if (ovl) group_overlap_launch<float>(gr, n, i + n < k);
+            if (ovl) n = std::min(s0->block, k - i);
+            if (ovl && s0->dtype == WS_F64) group_overlap_block<double>(gr, n, i == 0, i + n == k);
+            else if (ovl) group_overlap_block<float>(gr, n, i == 0, i + n == k);
             else if (s0->dtype == WS_F64) group_step<double>(gr, n);
             else group_step<float>(gr, n);
             for (ws_sim* s : gr->slabs)
@@ -396,6 +381,8 @@ int ws_group_run(ws_group_t* gr, int32_t n, int32_t* taken) {
                 }
             i += n;
         }
+        if (ovl)
+            for (ws_sim* s : gr->slabs) WS_HIP_CHECK(hipStreamWaitEvent(gr->stream, s->ev_edge, 0));
         WS_HIP_CHECK(hipEventRecord(s0->ev1, gr->stream));
         if (k > 0) {  // seam diagnostics need the neighbours' current rows (see run_steps)
             group_exchange(gr, 2, 1);
