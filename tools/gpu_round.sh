@@ -27,10 +27,11 @@ fail() { echo "step '$1' failed (rc=$2)"; exit "$2"; }
 
 for step in "$@"; do
   IFS=':' read -r name a1 a2 <<< "$step"
+  rest=""; [[ "$step" == *:* ]] && rest=${step#*:}   # everything after the step name
   echo "== $step"
   case "$name" in
     tests)
-      args=${a1//,/ }
+      args=${rest//,/ }
       timeout -k 10 ${PYTEST_T:-900} python -u -m pytest ${args:-tests} -m gpu -x -q --timeout 150 --timeout-method thread \
           > "$OUT/gpu_tests.log" 2>&1
       rc=$?; tail -3 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || fail "$step" $rc ;;
@@ -41,7 +42,7 @@ for step in "$@"; do
       timeout -k 10 400 python bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err"
       rc=$?; cut -c1-400 "$OUT/bench_default.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench_default.err"; fail "$step" $rc; } ;;
     configs)
-      list=${a1:-c1:rk4,c2:rk4,c2:rk2,c2:euler,c3:rk4,c4:rk4,c5:rk4,c2_slab2:rk4,c2_slab4:rk4,c2_slab8:rk4,c3p:rk4,c4p:rk4}
+      list=${rest:-c1:rk4,c2:rk4,c2:rk2,c2:euler,c3:rk4,c4:rk4,c5:rk4,c2_slab2:rk4,c2_slab4:rk4,c2_slab8:rk4,c3p:rk4,c4p:rk4}
       mkdir -p "$OUT/all"
       for spec in ${list//,/ }; do
         c=${spec%%:*}; m=${spec#*:}
