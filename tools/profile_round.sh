@@ -28,6 +28,10 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 "$R/bench.py" --config $CFG --method $METHOD --steps $STEPS --warmup $WARM --no-cpu-baseline --no-check --pin $PIN > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+# the kernels' VGPR / LDS / scratch as dispatched (tools/kernel_resources.py: the trace's VGPR
+# units corrected for gfx950)
+python3 "$R/tools/kernel_resources.py" "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" > "$OUT/kernel_resources.txt"
+head -3 "$OUT/kernel_resources.txt" | cut -c1-160
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT" "TCC_HIT_sum TCC_MISS_sum" \
@@ -42,4 +46,8 @@ python3 "$R/tools/traffic.py" "$OUT/pmc" "$KNAME" "$OUT/traffic_${CFG}_${METHOD}
 # the profiled variant: bench.py uses these counters only for runs of the same kernel and steps per launch
 python3 -c "
 import json; p='$OUT/traffic_${CFG}_${METHOD}.json'; d=json.load(open(p))
-d['variant'] = {'kernel': '$KERN', 'tb': $TB}; d['pin'] = '$PIN'; json.dump(d, open(p, 'w'))"
+d['variant'] = {'kernel': '$KERN', 'tb': $TB}; d['pin'] = '$PIN'
+import sys; sys.path.insert(0, '$R/tools'); import glob, kernel_resources as kr
+top = kr.summarize(glob.glob('$OUT/prof/**/*kernel_trace.csv', recursive=True)[0], '$KNAME')
+d['resources'] = top[0] if top else None
+json.dump(d, open(p, 'w'))"
