@@ -124,9 +124,10 @@ int fused_dppy_blocks_per_cu(int variant, int nstages, int nsteps, int sp_mode);
 // Strip geometry, per variant: columns per strip and the left margin (the dependency cone,
 // rounded up to whole 16-byte DMA chunks for the LDS-DMA variants: a strip's chunks then
 // never straddle column 0, where a partly negative chunk would be dropped whole by the
-// buffer range check). The output window of strip s is [s * out_w, (s + 1) * out_w); out_w
-// is at most columns - 2 * margin, and when `aligned` it is rounded down to whole 128-byte
-// lines so no two strips write parts of one line. (Variant ids are ABI values,
+// buffer range check). Middle strips output out_w columns, at most columns - 2 * margin, and
+// when `aligned` rounded down to whole 128-byte lines so no two strips write parts of one line;
+// the first and last strips lean on the global edges (strip_geom below). The lds variant keeps
+// the plain layout: strip s outputs [s * out_w, (s + 1) * out_w). (Variant ids are ABI values,
 // ws_sim_fused_variant; 1-3 belonged to variants removed after never winning a config.)
 enum FusedVariant : int { kFusedLds = 0, kFusedDppLdsY = 4, kFusedX2Y = 5, kFusedPc = 6, kFusedPc2 = 7 };
 // the variants of the wave-independent kernel (ws_fused_dppy_kernel.h), and their lane width
@@ -161,6 +162,42 @@ inline int fused_out_w(int variant, int nstages, int elem_bytes, bool aligned) {
     const int w = fused_strip_cols(variant) - 2 * fused_margin(variant, nstages, elem_bytes);
     const int line = 128 / elem_bytes;
     return aligned && w >= line ? w / line * line : w;
+}
+
+// Strip layout of the dppy family (round 5: edge-aware). A strip is a window of SW
+// (fused_strip_cols) columns whose outputs keep kM (fused_margin: the cone in whole 16-byte
+// chunks of kC columns) columns from the window's edges -- except at a global edge, where the
+// clamp takes the margin's place: the first strip's window starts at column 0 and the last
+// strip's is right-aligned to the row's end (rounded up to a chunk), so each outputs kM more
+// columns and a row may need one strip fewer (C4's 1024 columns: 9 pair strips instead of 10).
+// Middle strips output out_w columns. (With whole-line windows, out_w < SW - 2 kM, the first
+// strip outputs out_w columns too, keeping every middle window on 128-byte lines.)
+struct StripGeom {
+    int xs, o0, o1;  // window start column; output columns [o0, o1)
+};
+__host__ __device__ inline int strip_first_out(int SW, int kM, int out_w) {
+    return out_w == SW - 2 * kM ? SW - kM : out_w;
+}
+__host__ __device__ inline int strip_last_xs(int W, int SW, int kC) { return (W - SW + kC - 1) / kC * kC; }
+__host__ __device__ inline int strip_count(int W, int SW, int kM, int kC, int out_w) {
+    if (W <= SW) return 1;
+    const int need = strip_last_xs(W, SW, kC) + kM - strip_first_out(SW, kM, out_w);
+    return 2 + (need > 0 ? (need + out_w - 1) / out_w : 0);
+}
+__host__ __device__ inline StripGeom strip_geom(int s, int n, int W, int SW, int kM, int kC, int out_w) {
+    if (n == 1) return {0, 0, W};
+    const int first = strip_first_out(SW, kM, out_w);
+    if (s == 0) return {0, 0, first < W ? first : W};
+    const int o0 = first + (s - 1) * out_w;
+    if (s == n - 1) return {strip_last_xs(W, SW, kC), o0, W};
+    return {o0 - kM, o0, o0 + out_w < W ? o0 + out_w : W};
+}
+// the same for a launch: strips of a W-column row for variant / cone / element size / out_w
+inline int fused_strips(int variant, int W, int cone, int elem_bytes, int out_w) {
+    return strip_count(W, fused_strip_cols(variant), fused_margin(variant, cone, elem_bytes), 16 / elem_bytes, out_w);
+}
+inline StripGeom fused_strip_geom(int variant, int s, int n, int W, int cone, int elem_bytes, int out_w) {
+    return strip_geom(s, n, W, fused_strip_cols(variant), fused_margin(variant, cone, elem_bytes), 16 / elem_bytes, out_w);
 }
 
 }  // namespace ws

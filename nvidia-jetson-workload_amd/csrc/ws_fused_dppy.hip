@@ -19,7 +19,7 @@ hipError_t launch_fused_step_dppy(int variant, int nstages, int nsteps, const Fu
     if (out_w % (16 / (int)sizeof(T)) != 0) return hipErrorInvalidValue;  // chunk-aligned strips
     // column pairs are stored whole: an odd width's last pair ends in the row padding
     if (fused_pairs(variant) && (g.pitch % 2 != 0 || g.pitch < g.W + (g.W % 2))) return hipErrorInvalidValue;
-    const int nstrips = (g.W + out_w - 1) / out_w;
+    const int nstrips = fused_strips(variant, g.W, ns, (int)sizeof(T), out_w);
     const int nsegs = a.seg_n;
     if (a.chains ? a.nchains <= 0 : nsegs <= 0) return hipSuccess;
     const int64_t nblocks = a.chains ? (int64_t)a.nchains : (int64_t)nstrips * nsegs * g.L;

@@ -248,10 +248,12 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     constexpr int kC = 16 / (int)sizeof(T);  // columns per chunk
     constexpr int kM = (kNS + kC - 1) / kC * kC;
     const int out_w = a.out_w;
-    const int x = strip * out_w - kM + CPL * lane;  // this lane's (first) global column
+    // the strip's window and output columns (edge-aware layout, ws_fused.h strip_geom)
+    const StripGeom sg = strip_geom(strip, nstrips, g.W, kWave * CPL, kM, kC, out_w);
+    const int x = sg.xs + CPL * lane;  // this lane's (first) global column
     // a pair is stored whole: its second column is x + 1 < W, or row padding (x < W <= pitch,
     // both even), whose content is unspecified
-    const bool xout = x >= 0 && x < g.W && CPL * lane >= kM && CPL * lane < kM + out_w;
+    const bool xout = x >= sg.o0 && x < sg.o1;
     const XEdge xe{x == 0, x == g.W - 1, CPL == 2 && x + 1 == g.W - 1};
 
     const int row_lo = g.top_clamp ? 0 : -g.halo;  // rows that exist in memory (halo rows in slabs)
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // consecutive slots (64 lanes x 16 B = kG rows of the strip)
     __shared__ __attribute__((aligned(16))) VT ring[3][kNR][kWave];
     const int dk = lane / (kWave / kG);  // row of the group this lane fetches
-    const int dcol = (strip * out_w - kM) * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // 16-B aligned
+    const int dcol = sg.xs * (int)sizeof(T) + (lane % (kWave / kG)) * 16;  // 16-B aligned
     auto dma = [&](int q, int slot) {  // rows q .. q + kG - 1 into slots slot .. slot + kG - 1
         const int r = min(max(q + dk, row_lo), row_hi - 1);
         // chunks left of column 0 (whole chunks: kM is chunk-aligned) wrap to huge offsets or
@@ -558,8 +560,8 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         else if (producer) march_role(Xc, Yc, std::true_type{});
         else march_role(Xc, Yc, std::false_type{});
     };
-    // global edges matter only to strips / segments within kNS cells of them
-    const bool xclamp = strip == 0 || (strip + 1) * out_w >= g.W - kNS;
+    // global edges matter only to strips / segments whose outputs' cone (kNS cells) reaches them
+    const bool xclamp = sg.o0 <= kNS || sg.o1 + kNS >= g.W;
     const bool yclamp = (g.top_clamp && y0 < kNS) || (g.bot_clamp && y1 > g.H - kNS);
     if (xclamp) {
         if (yclamp) march(std::true_type{}, std::true_type{});

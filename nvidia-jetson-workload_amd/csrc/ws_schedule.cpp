@@ -99,7 +99,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     const int waves_per_wg = ws::fused_split(s->kernel) ? 2 : 1;
     const int64_t want = (int64_t)rounds * 4 * std::max(1, s->num_cus) / waves_per_wg;
     const int cone = nst * nsteps;
-    const int nstrips = (g->W + out_w - 1) / out_w;
+    const int nstrips = (int)ws::fused_strips(s->kernel, g->W, cone, (int)elem_size(s->dtype), out_w);
     struct Group {
         int unit;
         RowRange r;
@@ -113,7 +113,8 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
         for (int st = 0; st < nstrips; ++st)
             for (const RowRange& r : {A, B}) {
                 if (r.rows() <= 0) continue;
-                const bool xc = st == 0 || (st + 1) * out_w >= g->W - cone;  // the kernel's xclamp test
+                const ws::StripGeom sg = ws::fused_strip_geom(s->kernel, st, nstrips, g->W, cone, (int)elem_size(s->dtype), out_w);
+                const bool xc = sg.o0 <= cone || sg.o1 + cone >= g->W;  // the kernel's xclamp test
                 Group gr{l * nstrips + st, r, xc ? kXClampCost : 1.0};
                 total += gr.wx * r.rows();
                 groups.push_back(gr);

@@ -232,7 +232,10 @@ struct ws_sim {
 
     // cone = stages per launch (NST x steps per launch): the strip margins
     int out_w(int cone) const { return ws::fused_out_w(kernel, cone, (int)wsr::elem_size(dtype), align); }
-    int64_t strips(int cone) const { return (slot[0]->W + out_w(cone) - 1) / out_w(cone); }
+    int64_t strips(int cone) const {
+        return kernel == wsr::kKernLds ? (slot[0]->W + out_w(cone) - 1) / out_w(cone)
+                                       : ws::fused_strips(kernel, slot[0]->W, cone, (int)wsr::elem_size(dtype), out_w(cone));
+    }
     // steps per launch the tuned configuration launches where a run has room: tb, capped to
     // what the kernel takes at this integrator and precision (ws::fused_tb_ok: 4 -> 2 -> 1)
     int launch_tb() const;
