@@ -413,15 +413,15 @@ def lpe_words_per_cell(method):
     return sum(3 + 1 + 3 + acc_r + acc_w + 3 for acc_r, acc_w in stages)
 
 
-def bench_lpe(args, conf, method, world):
-    """Physics-mode layered primitive equations (config c4p), one GPU."""
+def bench_lpe(args, conf, method, world, rank=0, local=0, dist=None):
+    """Physics-mode layered primitive equations (config c4p): one GPU; `--slabs N` N slabs of
+    the ring decomposition on this GPU (one process, the pull transport); world > 1 one rank
+    per GPU (ws_lpe_create_slab, RCCL halos; strong scaling of the global grid)."""
     import numpy as np
     import torch
     import weather_sim as ws
     from oracle import layered_pe_oracle as lp
 
-    if world > 1:
-        raise SystemExit("c4p runs on one GPU")
     W, H, L = conf["W"], conf["H"], conf["L"]
     cfg = ws.SimulationConfig()
     cfg.grid_width, cfg.grid_height, cfg.num_levels = W, H, L
@@ -429,8 +429,18 @@ def bench_lpe(args, conf, method, world):
     cfg.double_precision = conf["fp64"]
     cfg.dx = cfg.dy = 1000.0
     cfg.dt, cfg.gravity, cfg.coriolis_f = 5.0, 9.81, 1e-4
+    cfg.device_id = local
     gp = 0.02
-    m = ws.LayeredPrimitiveEquationsModel(cfg, reduced_gravity=gp)
+    if world > 1:
+        m = ws.LayeredPrimitiveEquationsModel(cfg, reduced_gravity=gp,
+                                              slab=(rank, world, bootstrap_uid(dist, rank, ws.new_comm_id)))
+        parallelism = f"y-slabs over {world} GPUs (RCCL ring halos)"
+    elif args.slabs > 1:
+        m = ws.LayeredPrimitiveEquationsModel(cfg, reduced_gravity=gp, devices=[local] * args.slabs)
+        parallelism = f"{args.slabs} y-slabs on one GPU (one process, halo pull kernels)"
+    else:
+        m = ws.LayeredPrimitiveEquationsModel(cfg, reduced_gravity=gp)
+        parallelism = "single GPU"
 
     def initial(Wi, Hi):
         u, v, h = lp.rest_state(L, Hi, Wi, [40.0 + 2.0 * k for k in range(L)])
@@ -441,40 +451,49 @@ def bench_lpe(args, conf, method, world):
         return u, v, h
 
     s0 = initial(W, H)
-    m.set_state(*s0)
+    m.set_state(*(a[:, m.row0:m.row0 + m.rows] for a in s0))  # a rank's slab: its own rows
     if args.warmup > 0:
         m.run(args.warmup)
-    clock_ramp(lambda: m.run(2) or 2, None, args.warmup > 0)  # one GPU (world 1), as in main()
+    clock_ramp(lambda: m.run(2) or 2, dist if world > 1 else None, args.warmup > 0)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     m.run(args.steps)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(dist, elapsed)
     dev_ms, launches = m.last_run_stats()
     if not np.isfinite(m.get_field("h")).all():
         raise SystemExit("c4p: state is not finite after the timed run")
+    if rank != 0:
+        return
     w = 8 if conf["fp64"] else 4
     cells = W * H * L
-    step_bytes = lpe_words_per_cell(method) * w * cells
+    step_bytes = lpe_words_per_cell(method) * w * m.rows * W * L  # this rank's (or the whole) grid
     step_ms = dev_ms / args.steps
     achieved = step_bytes / (step_ms * 1e-3) / 1e9
     result = {
-        "metric": METRIC, "value": cells * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": 1,
+        "metric": METRIC, "value": cells * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "f64" if conf["fp64"] else "f32",
         "data": "synthetic (stacked layers with an interface wave), inputs resident in HBM",
         "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": L,
-                   "integrator": args.method, "parallelism": "single GPU"},
+                   "integrator": args.method, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _step_traffic(args, launches / args.steps),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": _step_traffic(args, launches / args.steps) if parallelism == "single GPU" else None,
                      "kernel": "lpe_stage_kernel (whole step)",
                      "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
                      "note": "device time of the run (hipEvents on the model's stream) per step; "
                              "bytes = lpe_words_per_cell x cells x levels"},
         "launches_per_step": launches / args.steps,
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         # the NumPy oracle (a port: no reference exists for this model) on a 256 x 256 x L
         # sample of the same per-cell work, bounded
         Ws = Hs = 256
@@ -536,6 +555,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--method", default="rk4", choices=sorted(METHODS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--slabs", type=int, default=1, help="c4p: N y-slabs of the ring decomposition on this GPU "
+                                                          "(one process; measures the decomposition's cost)")
     ap.add_argument("--no-check", action="store_true", help="skip the parity self-check (profiling runs)")
     ap.add_argument("--pin", default=None, help="kernel:steps_per_launch:seg_rows:align (profiling runs pin "
                                                 "the variant a bench run chose)")
@@ -567,7 +588,7 @@ def main():
     if args.config == "c3p":
         return bench_bvort(args, conf, method, world)
     if args.config == "c4p":
-        return bench_lpe(args, conf, method, world)
+        return bench_lpe(args, conf, method, world, rank, local, dist)
     cfg = ws.SimulationConfig()
     cfg.grid_width, cfg.grid_height, cfg.num_levels = conf["W"], conf["H"], conf["L"]
     cfg.model = conf["model"]

@@ -354,6 +354,33 @@ int ws_lpe_get_field(ws_lpe_t* model, int32_t field, void* host, int32_t levels,
 int ws_lpe_run(ws_lpe_t* model, int32_t num_steps);
 int ws_lpe_get_state(const ws_lpe_t* model, double* time, int32_t* step, double* last_run_ms,
                      int64_t* last_run_launches);
+/* y-slab decomposition of the layered model around its periodic ring (new): slab r owns the
+ * rows [row0, row0 + rows) of the balanced split (ws_slab_partition) with one halo row above
+ * and below every level, refreshed from the ring neighbours (slab 0's upper neighbour is the
+ * last slab) before every RK stage. Results are bitwise identical to ws_lpe_create's.
+ * ws_lpe_create_multi: ONE model over `ndevices` slabs in this process, slab r on devices[r]
+ * (entries may repeat: slabs sharing a device); halos pulled from the neighbours' memory by a
+ * copy kernel (peer access between distinct devices, else the runtime's 2-D copies). The
+ * handle is used like ws_lpe_create's: set / get_field take the whole (levels, height, width)
+ * field, run steps every slab. */
+int ws_lpe_create_multi(const ws_config_t* cfg, double reduced_gravity, const int32_t* devices, int32_t ndevices,
+                        ws_lpe_t** out);
+/* One rank of a process-per-GPU decomposition (device cfg->device_id): halos over RCCL
+ * (id from ws_comm_get_unique_id, the same bytes on every rank) with the periodic plan of
+ * ws_lpe_exchange_plan. Its set / get_field take the rank's own rows, (levels, rows, width);
+ * run() is collective. */
+int ws_lpe_create_slab(const ws_config_t* cfg, double reduced_gravity, int32_t rank, int32_t nranks,
+                       const uint8_t id[WS_COMM_ID_BYTES], ws_lpe_t** out, int32_t* row0, int32_t* rows);
+/* slabs of the decomposition (1: one domain) and this handle's global row range */
+int ws_lpe_layout(const ws_lpe_t* model, int32_t* nslabs, int32_t* row0, int32_t* rows);
+/* The periodic halo plan of rank `rank` (fields u, v, h; depth 1): like ws_slab_exchange_plan,
+ * but the ring closes (every rank has both neighbours when nranks > 1; with two ranks they are
+ * the same peer) and the slab layout is unpadded (pitch = width, level stride returned =
+ * (rows + 2) x width, one halo row). The transport posts the sends to side 0 (upper) and
+ * side 1 (lower), then the receives from side 1 and side 0, so a pair's k-th send meets the
+ * peer's k-th receive. */
+int ws_lpe_exchange_plan(int32_t width, int32_t rows, int32_t levels, int32_t dtype, int32_t rank, int32_t nranks,
+                         ws_xfer_t* out, int32_t capacity, int32_t* count, int64_t* level_stride);
 
 /* ---- per-kernel timing (measurement) --------------------------------------------- */
 /* When enabled, ws_sim_run / ws_sim_step time their kernels with hipEvents on the

@@ -43,12 +43,13 @@ SlabComm::~SlabComm() {
     if (scratch_) (void)hipFree(scratch_);
 }
 
-void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream) {
+void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream,
+                        bool periodic) {
     if (nranks_ == 1) return;
     if (nfields > kMaxHaloFields) throw CommError("too many fields for one exchange");
-    const HaloPlan plan = make_halo_plan(g, elem_size, rank_, nranks_, nfields, depth);
+    const HaloPlan plan = make_halo_plan(g, elem_size, rank_, nranks_, nfields, depth, periodic);
     const ncclComm_t c = (ncclComm_t)comm_;
-    if (halo_direct(plan)) {
+    if (halo_direct(plan) && !periodic) {
         // the plan executed literally: one send / receive per (field, level) segment, posted
         // in plan order (per neighbour: sends, then receives, field-major) on every rank, so
         // the k-th send to a peer meets that peer's k-th receive from us
@@ -67,12 +68,13 @@ void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const G
     for (int side = 0; side < 2; ++side)
         if (plan.has[side]) hcheck(halo_pack(plan, hf, side, staging_.send[side], stream), "halo_pack");
     const size_t bytes = (size_t)plan.msg_bytes();
+    // sends side 0, side 1, then receives side 1, side 0 (ws_halo.h: with a periodic ring of
+    // two ranks both sides are the same peer, and a pair's k-th send meets its k-th receive)
     check(ncclGroupStart(), "ncclGroupStart");
-    for (int side = 0; side < 2; ++side) {
-        if (!plan.has[side]) continue;
-        check(ncclSend(staging_.send[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclSend");
-        check(ncclRecv(staging_.recv[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclRecv");
-    }
+    for (int side = 0; side < 2; ++side)
+        if (plan.has[side]) check(ncclSend(staging_.send[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclSend");
+    for (int side = 1; side >= 0; --side)
+        if (plan.has[side]) check(ncclRecv(staging_.recv[side], bytes, ncclChar, plan.peer[side], c, stream), "ncclRecv");
     check(ncclGroupEnd(), "ncclGroupEnd");
     for (int side = 0; side < 2; ++side)
         if (plan.has[side]) hcheck(halo_unpack(plan, hf, side, staging_.recv[side], stream), "halo_unpack");

@@ -37,7 +37,9 @@ public:
     // Exchange `depth` halo rows of `nfields` level-stacked fields (row 0 of level 0 at
     // fields[i]) with both neighbours, enqueued on `stream`: pack each neighbour's segments
     // into one message (halo_pack), one grouped RCCL send / recv per neighbour, unpack.
-    void exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream);
+    // periodic: the ring closes (rank 0 <-> rank n-1; make_halo_plan), always packed.
+    void exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream,
+                  bool periodic = false);
     // rank `root`'s n int32 values to every rank (host in, host out; synchronises `stream`)
     void broadcast_i32(int32_t* v, int n, int root, hipStream_t stream);
     // In-place max over ranks of one double (device scratch owned by the comm).

@@ -12,7 +12,11 @@
 // buffer with halo_pack, move the message, and scatter it with halo_unpack -- so one plan
 // and one pair of kernels serve both, and the slab-group tests exercise them on the GPU.
 // The global top / bottom edges keep the reference's clamp-to-self stencil
-// (Geom::top_clamp / bot_clamp): no segment there.
+// (Geom::top_clamp / bot_clamp): no segment there. A periodic plan (the doubly periodic
+// layered model, ws_layered_pe.hip) closes the ring instead: rank 0's upper neighbour is rank
+// n-1 and rank n-1's lower one rank 0 -- with two ranks both neighbours are the same peer,
+// so the transports post the sends side 0 then side 1 and the receives side 1 then side 0:
+// a pair's k-th send meets the peer's k-th receive (my top rows -> its bottom halo first).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -49,7 +53,8 @@ struct HaloPlan {
     std::vector<HaloXfer> xfers() const;
 };
 
-HaloPlan make_halo_plan(const Geom& g, int elem_size, int rank, int nranks, int nfields, int depth);
+HaloPlan make_halo_plan(const Geom& g, int elem_size, int rank, int nranks, int nfields, int depth,
+                        bool periodic = false);
 
 // Transport choice: with few segments per neighbour (SWE: 3 fields x 1 level) each segment
 // moves by its own send / receive straight between the field rows (no pack / unpack

@@ -17,11 +17,14 @@
 // stage update (and the RK4 accumulator) in the same pass.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdlib>
 
 #include <string>
+#include <vector>
 
 #include "ws_abi.h"
+#include "ws_comm.h"
 #include "ws_hip.h"
 
 namespace ws {
@@ -45,7 +48,9 @@ struct LpeArgs {
     const T* tin;           // total thickness sum_k h_k of the input (H x W), or null: summed here
     T* tout;                // total thickness of the output h (summed in the walk), or null
     int W, H, L;
-    int64_t lstride;        // H * W
+    int64_t lstride;        // H * W; a slab: (H + 2) * W
+    int halo;               // 0: y wraps around H (the whole periodic domain); 1: a slab -- rows
+                            // -1 and H of every level are halo rows (the neighbours' edge rows)
     T c, w;
     int acc_mode;           // 0 none, 1 acc = w k, 2 acc += w k, 3 out = base + c (acc + k)
     T ix, iy;               // 1 / (2 dx), 1 / (2 dy)
@@ -101,13 +106,19 @@ void lpe_stage_kernel(LpeArgs<T> a) {
         const int lx = cc % kCX, ly = cc / kCX;
         int gx = (x0 + lx - 1) % a.W;
         if (gx < 0) gx += a.W;
-        int gy = (y0 + ly - 1) % a.H;
-        if (gy < 0) gy += a.H;
+        int gy = y0 + ly - 1;
+        if (a.halo) {
+            gy = gy > a.H ? a.H : gy;  // rows below the bottom halo row only feed cells outside the slab
+        } else {
+            gy %= a.H;
+            if (gy < 0) gy += a.H;
+        }
         hc[i] = a.h + (int64_t)gy * a.W + gx;
         T t = T(0);
         if (c < kCX * kCY) {
-            if (a.tin) {
-                // the producing stage summed the levels in the same order (bitwise the same)
+            if (a.tin && gy >= 0 && gy < a.H) {
+                // the producing stage summed the levels in the same order (bitwise the same);
+                // a slab's halo rows have no total here: summed below, in the same order
                 t = a.tin[(int64_t)gy * a.W + gx];
             } else {
 #pragma unroll 8
@@ -124,7 +135,8 @@ void lpe_stage_kernel(LpeArgs<T> a) {
     const int xc = inside ? x : 0, yc = inside ? y : 0;
     const int64_t oc = (int64_t)yc * a.W + xc;
     const int64_t oe = (int64_t)yc * a.W + wrapi(xc + 1, a.W), ow = (int64_t)yc * a.W + wrapi(xc - 1, a.W);
-    const int64_t on = (int64_t)wrapi(yc + 1, a.H) * a.W + xc, os = (int64_t)wrapi(yc - 1, a.H) * a.W + xc;
+    const int yn = a.halo ? yc + 1 : wrapi(yc + 1, a.H), ys = a.halo ? yc - 1 : wrapi(yc - 1, a.H);
+    const int64_t on = (int64_t)yn * a.W + xc, os = (int64_t)ys * a.W + xc;
     T tsum = T(0);  // total thickness of the output column, levels in order (as the scan sums)
     for (int k0 = 0; k0 < a.L; k0 += kChunk) {
         const int nk = a.L - k0 < kChunk ? a.L - k0 : kChunk;
@@ -207,6 +219,29 @@ void lpe_stage_kernel(LpeArgs<T> a) {
     if (a.tout && inside) a.tout[oc] = tsum;
 }
 
+// The halo rows of one slab of a one-process decomposition, pulled from its neighbours'
+// memory (same device, or a peer over xGMI): row -1 of every level of u, v, h <- the upper
+// neighbour's last row, row H <- the lower neighbour's row 0. grid (W / 256, L, 3 fields x 2).
+template <typename T>
+struct LpePull {
+    T* dst[3];
+    const T* up[3];
+    const T* dn[3];
+    int W, H, up_rows;
+    int64_t lstride, up_lstride, dn_lstride;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void lpe_pull_kernel(LpePull<T> a) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    if (x >= a.W) return;
+    const int l = blockIdx.y, f = blockIdx.z % 3, side = blockIdx.z / 3;
+    const T* src = side == 0 ? a.up[f] + (int64_t)l * a.up_lstride + (int64_t)(a.up_rows - 1) * a.W
+                             : a.dn[f] + (int64_t)l * a.dn_lstride;
+    T* dst = a.dst[f] + (int64_t)l * a.lstride + (side == 0 ? -(int64_t)a.W : (int64_t)a.H * a.W);
+    dst[x] = src[x];
+}
+
 void hck(hipError_t e, const char* what) {
     if (e != hipSuccess) throw AbiError(WS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -220,6 +255,7 @@ struct ws_lpe {
     int32_t step = 0;
     hipStream_t stream = nullptr;
     // state slots, stage buffers A / B and the RK4 accumulator: 3 fields each, [L][H][W]
+    // (a slab: [L][H + 2][W], the pointers at row 0 of level 0, rows -1 and H the halo)
     void* S[2][3] = {};
     void* A[3] = {};
     void* B[3] = {};
@@ -233,27 +269,102 @@ struct ws_lpe {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
     int64_t launches = 0;
+    // y-slab decomposition around the periodic ring (ws_lpe_create_multi / _create_slab): this
+    // model owns global rows [row0, row0 + H) of Hg; halo = 1 gives every level a halo row
+    // above and below, refreshed before every RK stage -- from the neighbours' memory by the
+    // process's own kernels (parts of a one-process decomposition) or over RCCL (comm)
+    int Hg = 0, row0 = 0, halo = 0;
+    int rank = 0, nranks = 1;
+    ws::SlabComm* comm = nullptr;
+    std::vector<ws_lpe*> parts;     // a one-process decomposition: its slabs (it holds no buffers itself)
+    hipEvent_t ev_stage = nullptr;  // a part: recorded after its latest stage kernel
+    bool pull_direct = true;        // a part: the pull kernel may read both neighbours' memory
     size_t es() const { return dtype == WS_F64 ? 8 : 4; }
     size_t cells() const { return (size_t)L * H * W; }
+    int64_t lstride() const { return (int64_t)(H + 2 * halo) * W; }
+    size_t alloc_bytes() const { return (size_t)L * lstride() * es(); }
+    size_t halo_bytes() const { return (size_t)halo * W * es(); }
 };
 
 namespace ws {
 namespace {
 
 void lpe_free(ws_lpe* m) {
+    for (ws_lpe* p : m->parts) {
+        (void)hipSetDevice(p->device);
+        lpe_free(p);
+    }
+    m->parts.clear();
     if (m->stream) (void)hipStreamSynchronize(m->stream);  // nothing queued may touch freed memory
+    auto field_free = [&](void* p) {
+        if (p) (void)hipFree((char*)p - m->halo_bytes());
+    };
     for (int s = 0; s < 2; ++s)
-        for (void* p : m->S[s])
-            if (p) (void)hipFree(p);
+        for (void* p : m->S[s]) field_free(p);
     for (void** grp : {m->A, m->B, m->acc})
-        for (int i = 0; i < 3; ++i)
-            if (grp[i]) (void)hipFree(grp[i]);
+        for (int i = 0; i < 3; ++i) field_free(grp[i]);
     for (void* p : m->tot)
         if (p) (void)hipFree(p);
-    for (hipEvent_t e : {m->ev0, m->ev1})
+    for (hipEvent_t e : {m->ev0, m->ev1, m->ev_stage})
         if (e) (void)hipEventDestroy(e);
     if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m->comm;
     delete m;
+}
+
+// the model parameters of cfg (no buffers)
+void lpe_params(ws_lpe* m, const ws_config_t* cfg, double gp) {
+    m->W = cfg->grid_width;
+    m->H = m->Hg = cfg->grid_height;
+    m->L = cfg->num_levels;
+    m->dtype = cfg->double_precision ? WS_F64 : WS_F32;
+    m->device = cfg->device_id;
+    m->method = cfg->integration_method == WS_RK2 ? WS_RK2 : cfg->integration_method == WS_RK4 ? WS_RK4 : WS_EULER;
+    m->dx = cfg->dx;
+    m->dy = cfg->dy;
+    m->dt = cfg->dt;
+    m->g = cfg->gravity;
+    m->f = cfg->coriolis_f;
+    m->gp = gp;
+}
+
+void lpe_check_config(const ws_config_t* cfg) {
+    if (cfg->grid_width < 3 || cfg->grid_height < 3 || cfg->num_levels < 1)
+        throw AbiError(WS_ERR_INVALID, "layered model needs a grid of at least 3 x 3 and one layer");
+    if (!(cfg->dx > 0 && cfg->dy > 0)) throw AbiError(WS_ERR_INVALID, "Grid spacing must be positive");
+}
+
+// stream, events and zeroed buffers of a model whose geometry (W, H, L, halo) is set; the
+// device is current
+void lpe_alloc(ws_lpe* m) {
+    hck(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking), "hipStreamCreate");
+    hck(hipEventCreate(&m->ev0), "hipEventCreate");
+    hck(hipEventCreate(&m->ev1), "hipEventCreate");
+    hck(hipEventCreateWithFlags(&m->ev_stage, hipEventDisableTiming), "hipEventCreate");
+    auto field = [&](void*& p) {
+        void* a = nullptr;
+        hck(hipMalloc(&a, m->alloc_bytes()), "hipMalloc");
+        p = (char*)a + m->halo_bytes();
+        hck(hipMemsetAsync(a, 0, m->alloc_bytes(), m->stream), "hipMemsetAsync");
+    };
+    for (int s = 0; s < 2; ++s)
+        for (void*& p : m->S[s]) field(p);
+    for (void** grp : {m->A, m->B, m->acc})
+        for (int i = 0; i < 3; ++i) field(grp[i]);
+    for (void*& p : m->tot) hck(hipMalloc(&p, (size_t)m->H * m->W * m->es()), "hipMalloc");
+    // the field uploads (ws_lpe_set_field) use hipMemcpy, which is not ordered with the
+    // model's non-blocking stream: the zeroing must be complete first
+    hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
+}
+
+// field sets by id: 0 the current state, 1 the next, 2 A, 3 B
+void* const* set_of(ws_lpe* m, int id) {
+    switch (id) {
+        case 0: return m->S[m->cur];
+        case 1: return m->S[1 - m->cur];
+        case 2: return m->A;
+        default: return m->B;
+    }
 }
 
 // index of a field set's total-thickness buffer: S[0], S[1], A, B
@@ -287,7 +398,8 @@ void stage(ws_lpe* m, void* const* in, void* const* out, T c, T w, int acc_mode)
     a.W = m->W;
     a.H = m->H;
     a.L = m->L;
-    a.lstride = (int64_t)m->H * m->W;
+    a.lstride = m->lstride();
+    a.halo = m->halo;
     a.c = c;
     a.w = w;
     a.acc_mode = acc_mode;
@@ -302,27 +414,98 @@ void stage(ws_lpe* m, void* const* in, void* const* out, T c, T w, int acc_mode)
     m->launches += 1;
 }
 
+// part p's halo rows of field set `sid` from its ring neighbours (one-process decomposition),
+// on p's stream once the neighbours' previous stages are done
+template <typename T>
+void pull_halo(ws_lpe* m, int p, int sid) {
+    const int n = (int)m->parts.size();
+    ws_lpe* me = m->parts[p];
+    ws_lpe* up = m->parts[(p + n - 1) % n];
+    ws_lpe* dn = m->parts[(p + 1) % n];
+    hck(hipStreamWaitEvent(me->stream, up->ev_stage, 0), "hipStreamWaitEvent");
+    if (dn != up) hck(hipStreamWaitEvent(me->stream, dn->ev_stage, 0), "hipStreamWaitEvent");
+    void* const* d = set_of(me, sid);
+    void* const* u = set_of(up, sid);
+    void* const* w = set_of(dn, sid);
+    if (me->pull_direct) {
+        LpePull<T> a{};
+        for (int f = 0; f < 3; ++f) {
+            a.dst[f] = (T*)d[f];
+            a.up[f] = (const T*)u[f];
+            a.dn[f] = (const T*)w[f];
+        }
+        a.W = me->W;
+        a.H = me->H;
+        a.up_rows = up->H;
+        a.lstride = me->lstride();
+        a.up_lstride = up->lstride();
+        a.dn_lstride = dn->lstride();
+        hipLaunchKernelGGL((lpe_pull_kernel<T>), dim3((me->W + 255) / 256, me->L, 6), dim3(256), 0, me->stream, a);
+        hck(hipGetLastError(), "lpe_pull_kernel");
+        me->launches += 1;
+        return;
+    }
+    // no peer access between the devices: the runtime's 2-D copies (L rows of W each)
+    const size_t row = (size_t)me->W * sizeof(T);
+    for (int f = 0; f < 3; ++f) {
+        hck(hipMemcpy2DAsync((char*)d[f] - row, me->lstride() * sizeof(T), (const char*)u[f] + (up->H - 1) * row,
+                             up->lstride() * sizeof(T), row, me->L, hipMemcpyDefault, me->stream),
+            "hipMemcpy2DAsync");
+        hck(hipMemcpy2DAsync((char*)d[f] + me->H * row, me->lstride() * sizeof(T), w[f], dn->lstride() * sizeof(T),
+                             row, me->L, hipMemcpyDefault, me->stream),
+            "hipMemcpy2DAsync");
+    }
+}
+
+// one RK stage of the model -- every part of a one-process decomposition (halo pulls for all
+// of them first: a part's pull must not see a neighbour's event of this same stage), or a
+// process's slab after its RCCL exchange, or the whole domain
+template <typename T>
+void stage_all(ws_lpe* m, int in_id, int out_id, T c, T w, int acc_mode) {
+    if (m->parts.empty()) {
+        if (m->comm && m->nranks > 1) {
+            Geom g{};
+            g.W = m->W; g.H = m->H; g.L = m->L;
+            g.pitch = m->W;
+            g.lstride = m->lstride();
+            g.halo = 1;
+            m->comm->exchange(set_of(m, in_id), 3, (int)sizeof(T), g, 1, m->stream, /*periodic=*/true);
+        }
+        stage<T>(m, set_of(m, in_id), set_of(m, out_id), c, w, acc_mode);
+        return;
+    }
+    const int n = (int)m->parts.size();
+    for (int p = 0; p < n; ++p) {
+        hck(hipSetDevice(m->parts[p]->device), "hipSetDevice");
+        pull_halo<T>(m, p, in_id);
+    }
+    for (ws_lpe* p : m->parts) {
+        hck(hipSetDevice(p->device), "hipSetDevice");
+        stage<T>(p, set_of(p, in_id), set_of(p, out_id), c, w, acc_mode);
+        hck(hipEventRecord(p->ev_stage, p->stream), "hipEventRecord");
+    }
+}
+
 template <typename T>
 void enqueue_step(ws_lpe* m) {
     const T dt = (T)m->dt;
-    void* const* y0 = m->S[m->cur];
-    void* const* y1 = m->S[1 - m->cur];
     switch (m->method) {
         case WS_RK2:
-            stage<T>(m, y0, m->A, T(0.5) * dt, T(0), 0);
-            stage<T>(m, m->A, y1, dt, T(0), 0);
+            stage_all<T>(m, 0, 2, T(0.5) * dt, T(0), 0);
+            stage_all<T>(m, 2, 1, dt, T(0), 0);
             break;
         case WS_RK4:
-            stage<T>(m, y0, m->A, T(0.5) * dt, T(1), 1);
-            stage<T>(m, m->A, m->B, T(0.5) * dt, T(2), 2);
-            stage<T>(m, m->B, m->A, dt, T(2), 2);
-            stage<T>(m, m->A, y1, dt / T(6), T(0), 3);
+            stage_all<T>(m, 0, 2, T(0.5) * dt, T(1), 1);
+            stage_all<T>(m, 2, 3, T(0.5) * dt, T(2), 2);
+            stage_all<T>(m, 3, 2, dt, T(2), 2);
+            stage_all<T>(m, 2, 1, dt / T(6), T(0), 3);
             break;
         default:
-            stage<T>(m, y0, y1, dt, T(0), 0);
+            stage_all<T>(m, 0, 1, dt, T(0), 0);
             break;
     }
     m->cur = 1 - m->cur;
+    for (ws_lpe* p : m->parts) p->cur = 1 - p->cur;
 }
 
 void check_field_call(const ws_lpe* m, const void* host, int32_t field, int32_t levels, int32_t height, int32_t width,
@@ -331,6 +514,63 @@ void check_field_call(const ws_lpe* m, const void* host, int32_t field, int32_t 
     if (field < 0 || field > 2) throw AbiError(WS_ERR_INVALID, "bad field id");
     if (levels != m->L || height != m->H || width != m->W) throw AbiError(WS_ERR_SHAPE, "array shape mismatch");
     if (dtype != m->dtype) throw AbiError(WS_ERR_INVALID, "dtype must match the model precision");
+}
+
+// host (L, rows, W) rows [r0, r0 + p->H) of every level <-> part p's own rows
+void copy_field(ws_lpe* p, int32_t field, void* host, int host_rows, int r0, bool upload) {
+    abi_set_device(p->device);
+    hck(hipStreamSynchronize(p->stream), "hipStreamSynchronize");
+    const size_t row = (size_t)p->W * p->es();
+    char* h = (char*)host + (size_t)r0 * row;
+    char* d = (char*)p->S[p->cur][field];
+    const size_t hpitch = (size_t)host_rows * row, dpitch = (size_t)p->lstride() * p->es();
+    if (upload) {
+        hck(hipMemcpy2D(d, dpitch, h, hpitch, p->H * row, p->L, hipMemcpyHostToDevice), "hipMemcpy2D");
+        p->tot_ok[p->cur] = false;  // the next stage sums the new thickness itself
+    } else {
+        hck(hipMemcpy2D(h, hpitch, d, dpitch, p->H * row, p->L, hipMemcpyDeviceToHost), "hipMemcpy2D");
+    }
+}
+
+void transfer(ws_lpe* m, int32_t field, void* host, bool upload) {
+    if (m->parts.empty()) {
+        copy_field(m, field, host, m->H, 0, upload);
+        return;
+    }
+    for (ws_lpe* p : m->parts) copy_field(p, field, host, m->H, p->row0, upload);
+}
+
+// one slab of the ring: rows [row0, row0 + rows) of cfg's grid, halo rows when nranks > 1
+ws_lpe* lpe_make(const ws_config_t* cfg, double gp, int device, int rank, int nranks) {
+    ws_lpe* m = new ws_lpe;
+    lpe_params(m, cfg, gp);
+    m->device = device;
+    m->rank = rank;
+    m->nranks = nranks;
+    slab_rows(m->Hg, rank, nranks, &m->row0, &m->H);
+    m->halo = nranks > 1 ? 1 : 0;
+    try {
+        abi_set_device(device);
+        lpe_alloc(m);
+    } catch (...) {
+        lpe_free(m);
+        throw;
+    }
+    return m;
+}
+
+// peer access from `dev` to `peer` (already enabled counts); false where the devices cannot
+bool enable_peer(int dev, int peer) {
+    if (dev == peer) return true;
+    int ok = 0;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) return false;
+    hck(hipSetDevice(dev), "hipSetDevice");
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return e == hipSuccess;
 }
 
 }  // namespace
@@ -343,39 +583,38 @@ extern "C" {
 int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out) {
     return ws::abi_guarded([&] {
         if (!cfg || !out) throw AbiError(WS_ERR_INVALID, "null argument");
-        if (cfg->grid_width < 3 || cfg->grid_height < 3 || cfg->num_levels < 1)
-            throw AbiError(WS_ERR_INVALID, "layered model needs a grid of at least 3 x 3 and one layer");
-        if (!(cfg->dx > 0 && cfg->dy > 0)) throw AbiError(WS_ERR_INVALID, "Grid spacing must be positive");
-        ws::abi_set_device(cfg->device_id);
+        ws::lpe_check_config(cfg);
+        *out = ws::lpe_make(cfg, reduced_gravity, cfg->device_id, 0, 1);
+    });
+}
+
+int ws_lpe_create_multi(const ws_config_t* cfg, double reduced_gravity, const int32_t* devices, int32_t ndevices,
+                        ws_lpe_t** out) {
+    return ws::abi_guarded([&] {
+        if (!cfg || !out || !devices) throw AbiError(WS_ERR_INVALID, "null argument");
+        ws::lpe_check_config(cfg);
+        if (ndevices < 1 || ndevices > cfg->grid_height)
+            throw AbiError(WS_ERR_INVALID, "need 1 <= slabs <= grid_height");
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+        for (int i = 0; i < ndevices; ++i)
+            if (devices[i] < 0 || devices[i] >= count) throw AbiError(WS_ERR_DEVICE, "no such device");
+        if (ndevices == 1) {
+            *out = ws::lpe_make(cfg, reduced_gravity, devices[0], 0, 1);
+            return;
+        }
         ws_lpe* m = new ws_lpe;
-        m->W = cfg->grid_width;
-        m->H = cfg->grid_height;
-        m->L = cfg->num_levels;
-        m->dtype = cfg->double_precision ? WS_F64 : WS_F32;
-        m->device = cfg->device_id;
-        m->method = cfg->integration_method == WS_RK2 ? WS_RK2 : cfg->integration_method == WS_RK4 ? WS_RK4 : WS_EULER;
-        m->dx = cfg->dx;
-        m->dy = cfg->dy;
-        m->dt = cfg->dt;
-        m->g = cfg->gravity;
-        m->f = cfg->coriolis_f;
-        m->gp = reduced_gravity;
+        ws::lpe_params(m, cfg, reduced_gravity);
+        m->device = devices[0];
+        m->nranks = ndevices;
         try {
-            ws::hck(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking), "hipStreamCreate");
-            ws::hck(hipEventCreate(&m->ev0), "hipEventCreate");
-            ws::hck(hipEventCreate(&m->ev1), "hipEventCreate");
-            const size_t fb = m->cells() * m->es();
-            for (int s = 0; s < 2; ++s)
-                for (void*& p : m->S[s]) {
-                    ws::hck(hipMalloc(&p, fb), "hipMalloc");
-                    ws::hck(hipMemsetAsync(p, 0, fb, m->stream), "hipMemsetAsync");
-                }
-            // the field uploads (ws_lpe_set_field) use hipMemcpy, which is not ordered with the
-            // model's non-blocking stream: the zeroing must be complete first
-            ws::hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
-            for (void** grp : {m->A, m->B, m->acc})
-                for (int i = 0; i < 3; ++i) ws::hck(hipMalloc(&grp[i], fb), "hipMalloc");
-            for (void*& p : m->tot) ws::hck(hipMalloc(&p, (size_t)m->H * m->W * m->es()), "hipMalloc");
+            for (int r = 0; r < ndevices; ++r)
+                m->parts.push_back(ws::lpe_make(cfg, reduced_gravity, devices[r], r, ndevices));
+            for (int r = 0; r < ndevices; ++r) {
+                ws_lpe* p = m->parts[r];
+                const int up = devices[(r + ndevices - 1) % ndevices], dn = devices[(r + 1) % ndevices];
+                p->pull_direct = ws::enable_peer(p->device, up) && ws::enable_peer(p->device, dn);
+            }
         } catch (...) {
             ws::lpe_free(m);
             throw;
@@ -384,11 +623,67 @@ int ws_lpe_create(const ws_config_t* cfg, double reduced_gravity, ws_lpe_t** out
     });
 }
 
+int ws_lpe_create_slab(const ws_config_t* cfg, double reduced_gravity, int32_t rank, int32_t nranks,
+                       const uint8_t id[WS_COMM_ID_BYTES], ws_lpe_t** out, int32_t* row0, int32_t* rows) {
+    return ws::abi_guarded([&] {
+        if (!cfg || !out || !id) throw AbiError(WS_ERR_INVALID, "null argument");
+        ws::lpe_check_config(cfg);
+        if (nranks < 1 || rank < 0 || rank >= nranks || nranks > cfg->grid_height)
+            throw AbiError(WS_ERR_INVALID, "bad rank / nranks");
+        ws_lpe* m = ws::lpe_make(cfg, reduced_gravity, cfg->device_id, rank, nranks);
+        try {
+            // a 1-rank slab gets its communicator too (the exchanges are no-ops): the RCCL
+            // bootstrap runs on one GPU
+            m->comm = new ws::SlabComm(rank, nranks, id);
+        } catch (const std::exception& e) {
+            ws::lpe_free(m);
+            throw AbiError(WS_ERR_DEVICE, e.what());
+        }
+        *out = m;
+        if (row0) *row0 = m->row0;
+        if (rows) *rows = m->H;
+    });
+}
+
+int ws_lpe_layout(const ws_lpe_t* m, int32_t* nslabs, int32_t* row0, int32_t* rows) {
+    return ws::abi_guarded([&] {
+        if (!m) throw AbiError(WS_ERR_INVALID, "null model");
+        if (nslabs) *nslabs = m->nranks;
+        if (row0) *row0 = m->row0;
+        if (rows) *rows = m->H;
+    });
+}
+
+int ws_lpe_exchange_plan(int32_t width, int32_t rows, int32_t levels, int32_t dtype, int32_t rank, int32_t nranks,
+                         ws_xfer_t* out, int32_t capacity, int32_t* count, int64_t* level_stride) {
+    return ws::abi_guarded([&] {
+        if (width < 1 || rows < 1 || levels < 1) throw AbiError(WS_ERR_INVALID, "Grid dimensions must be positive");
+        if (dtype != WS_F32 && dtype != WS_F64) throw AbiError(WS_ERR_INVALID, "bad dtype");
+        if (nranks < 1 || rank < 0 || rank >= nranks) throw AbiError(WS_ERR_INVALID, "bad rank / nranks");
+        // a slab's layout (lpe_alloc): unpadded rows, one halo row above and below every level
+        ws::Geom g{};
+        g.W = width; g.H = rows; g.L = levels;
+        g.pitch = width;
+        g.lstride = (int64_t)(rows + 2) * width;
+        g.halo = 1;
+        const auto x = ws::make_halo_plan(g, dtype == WS_F64 ? 8 : 4, rank, nranks, 3, 1, true).xfers();
+        if (count) *count = (int32_t)x.size();
+        if (level_stride) *level_stride = g.lstride;
+        if (out) {
+            if (capacity < (int32_t)x.size()) throw AbiError(WS_ERR_INVALID, "plan capacity too small");
+            for (size_t i = 0; i < x.size(); ++i) {
+                out[i].peer = x[i].peer; out[i].kind = x[i].kind; out[i].field = x[i].field;
+                out[i].level = x[i].level; out[i].offset = x[i].offset; out[i].bytes = x[i].bytes;
+                out[i].msg_offset = x[i].msg_offset;
+            }
+        }
+    });
+}
+
 int ws_lpe_destroy(ws_lpe_t* m) {
     return ws::abi_guarded([&] {
         if (!m) return;
         (void)hipSetDevice(m->device);
-        (void)hipStreamSynchronize(m->stream);
         ws::lpe_free(m);
     });
 }
@@ -397,10 +692,7 @@ int ws_lpe_set_field(ws_lpe_t* m, int32_t field, const void* host, int32_t level
                      int32_t dtype) {
     return ws::abi_guarded([&] {
         ws::check_field_call(m, host, field, levels, height, width, dtype);
-        ws::abi_set_device(m->device);
-        ws::hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
-        ws::hck(hipMemcpy(m->S[m->cur][field], host, m->cells() * m->es(), hipMemcpyHostToDevice), "hipMemcpy");
-        m->tot_ok[m->cur] = false;  // the next stage sums the new thickness itself
+        ws::transfer(m, field, const_cast<void*>(host), true);
     });
 }
 
@@ -408,9 +700,7 @@ int ws_lpe_get_field(ws_lpe_t* m, int32_t field, void* host, int32_t levels, int
                      int32_t dtype) {
     return ws::abi_guarded([&] {
         ws::check_field_call(m, host, field, levels, height, width, dtype);
-        ws::abi_set_device(m->device);
-        ws::hck(hipStreamSynchronize(m->stream), "hipStreamSynchronize");
-        ws::hck(hipMemcpy(host, m->S[m->cur][field], m->cells() * m->es(), hipMemcpyDeviceToHost), "hipMemcpy");
+        ws::transfer(m, field, host, false);
     });
 }
 
@@ -418,9 +708,14 @@ int ws_lpe_run(ws_lpe_t* m, int32_t n) {
     return ws::abi_guarded([&] {
         if (!m) throw AbiError(WS_ERR_INVALID, "null model");
         if (n <= 0) return;
-        ws::abi_set_device(m->device);
         m->launches = 0;
-        ws::hck(hipEventRecord(m->ev0, m->stream), "hipEventRecord");
+        for (ws_lpe* p : m->parts) p->launches = 0;
+        // one-process decomposition: host time from the first enqueue to the last part's end
+        const auto t0 = std::chrono::steady_clock::now();
+        if (m->parts.empty()) {
+            ws::abi_set_device(m->device);
+            ws::hck(hipEventRecord(m->ev0, m->stream), "hipEventRecord");
+        }
         for (int i = 0; i < n; ++i) {
             if (m->dtype == WS_F64) {
                 ws::enqueue_step<double>(m);
@@ -431,11 +726,20 @@ int ws_lpe_run(ws_lpe_t* m, int32_t n) {
             }
             m->step++;
         }
-        ws::hck(hipEventRecord(m->ev1, m->stream), "hipEventRecord");
-        ws::hck(hipEventSynchronize(m->ev1), "hipEventSynchronize");
-        float ms = 0.f;
-        ws::hck(hipEventElapsedTime(&ms, m->ev0, m->ev1), "hipEventElapsedTime");
-        m->last_ms = ms;
+        if (m->parts.empty()) {
+            ws::hck(hipEventRecord(m->ev1, m->stream), "hipEventRecord");
+            ws::hck(hipEventSynchronize(m->ev1), "hipEventSynchronize");
+            float ms = 0.f;
+            ws::hck(hipEventElapsedTime(&ms, m->ev0, m->ev1), "hipEventElapsedTime");
+            m->last_ms = ms;
+            return;
+        }
+        for (ws_lpe* p : m->parts) {
+            ws::hck(hipSetDevice(p->device), "hipSetDevice");
+            ws::hck(hipStreamSynchronize(p->stream), "hipStreamSynchronize");
+            m->launches += p->launches;
+        }
+        m->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
 

@@ -158,6 +158,10 @@ SIGNATURES = {
     "ws_lpe_get_field": [_P, _I, _P, _I, _I, _I, _I],
     "ws_lpe_run": [_P, _I],
     "ws_lpe_get_state": [_P, _PD, _PI, _PD, _PL],
+    "ws_lpe_create_multi": [ctypes.POINTER(ws_config_t), _D, _PI, _I, _PP],
+    "ws_lpe_create_slab": [ctypes.POINTER(ws_config_t), _D, _I, _I, ctypes.POINTER(ctypes.c_uint8), _PP, _PI, _PI],
+    "ws_lpe_layout": [_P, _PI, _PI, _PI],
+    "ws_lpe_exchange_plan": [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ws_xfer_t), _I, _PI, _PL],
 }
 _RESTYPES = {"ws_last_error": ctypes.c_char_p, "ws_config_default": None}
 
@@ -222,3 +226,15 @@ def exchange_plan(width, rows, levels, fp64, rank, nranks, nfields, depth):
     check(lib.ws_slab_exchange_plan(width, rows, levels, dt, rank, nranks, nfields, depth, buf, n.value,
                                     ctypes.byref(n), None, None))
     return list(buf[:n.value]), pitch.value, lstride.value
+
+
+def lpe_exchange_plan(width, rows, levels, fp64, rank, nranks):
+    """The layered model's periodic halo plan (ws_lpe_exchange_plan): (list of ws_xfer_t,
+    level_stride) for one slab of the ring (pitch = width, one halo row)."""
+    n, lstride = ctypes.c_int32(0), ctypes.c_int64(0)
+    dt = WS_F64 if fp64 else WS_F32
+    check(lib.ws_lpe_exchange_plan(width, rows, levels, dt, rank, nranks, None, 0, ctypes.byref(n),
+                                   ctypes.byref(lstride)))
+    buf = (ws_xfer_t * max(1, n.value))()
+    check(lib.ws_lpe_exchange_plan(width, rows, levels, dt, rank, nranks, buf, n.value, ctypes.byref(n), None))
+    return list(buf[:n.value]), lstride.value

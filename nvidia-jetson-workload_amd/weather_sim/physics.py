@@ -133,18 +133,54 @@ class LayeredPrimitiveEquationsModel:
     weather_simulation.cpp:542-560; `WeatherSimulation` reproduces that bit for bit). Defined
     by oracle/layered_pe_oracle.py; g = config.gravity, f = config.coriolis_f,
     g' = `reduced_gravity`. Fields are (levels, height, width) arrays; h is layer thickness.
+
+    Slab decomposition (y-slabs around the periodic ring, one halo row per level refreshed
+    before every RK stage; bitwise identical to one domain):
+      * `devices=[d0, d1, ...]` (or `config.devices` with more than one entry): one model over
+        len(devices) slabs in this process, slab r on devices[r] (repeats share a device);
+        the API is unchanged -- fields are the whole (levels, height, width) arrays;
+      * `slab=(rank, nranks, comm_id)`: one rank of a process-per-GPU decomposition over RCCL
+        (`comm_id` from weather_sim.new_comm_id() on one rank, the same bytes everywhere);
+        fields are the rank's rows, (levels, rows, width), rows [row0, row0 + rows); run() is
+        collective.
     """
 
-    def __init__(self, config, reduced_gravity=0.05):
+    def __init__(self, config, reduced_gravity=0.05, devices=None, slab=None):
+        from ._native import COMM_ID_BYTES
         from .weather_simulation import SimulationConfig
         if not isinstance(config, SimulationConfig):
             raise TypeError("LayeredPrimitiveEquationsModel expects a SimulationConfig")
         raw = config._to_c()
         h = ctypes.c_void_p()
-        check(lib.ws_lpe_create(ctypes.byref(raw), float(reduced_gravity), ctypes.byref(h)))
+        if devices is None and slab is None and len(getattr(config, "devices", None) or ()) > 1:
+            devices = config.devices
+        if devices is not None and slab is not None:
+            raise ValueError("devices= and slab= are exclusive")
+        if slab is not None:
+            rank, nranks, comm_id = slab
+            if comm_id is None or len(comm_id) != COMM_ID_BYTES:
+                raise ValueError(f"comm_id must be {COMM_ID_BYTES} bytes (weather_sim.new_comm_id())")
+            idb = (ctypes.c_uint8 * COMM_ID_BYTES)(*comm_id)
+            r0, nr = ctypes.c_int32(), ctypes.c_int32()
+            check(lib.ws_lpe_create_slab(ctypes.byref(raw), float(reduced_gravity), int(rank), int(nranks), idb,
+                                         ctypes.byref(h), ctypes.byref(r0), ctypes.byref(nr)))
+        elif devices is not None:
+            devs = [int(d) for d in devices]
+            if not devs:
+                raise ValueError("devices must name at least one device")
+            arr = (ctypes.c_int32 * len(devs))(*devs)
+            check(lib.ws_lpe_create_multi(ctypes.byref(raw), float(reduced_gravity), arr, len(devs),
+                                          ctypes.byref(h)))
+        else:
+            check(lib.ws_lpe_create(ctypes.byref(raw), float(reduced_gravity), ctypes.byref(h)))
         self._h = h
+        ns, r0, nr = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_lpe_layout(self._h, ctypes.byref(ns), ctypes.byref(r0), ctypes.byref(nr)))
+        self.nslabs, self.row0, self.rows = ns.value, r0.value, nr.value
         self.levels = int(config.num_levels)
-        self.width, self.height = int(config.grid_width), int(config.grid_height)
+        # a process's slab holds its own rows only
+        self.width, self.height = int(config.grid_width), self.rows
+        self.global_height = int(config.grid_height)
         self.dtype = np.float64 if config.double_precision else np.float32
         self.reduced_gravity = float(reduced_gravity)
 
