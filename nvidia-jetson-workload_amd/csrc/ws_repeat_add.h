@@ -14,6 +14,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #ifndef WS_HD
 #if defined(__HIPCC__)
@@ -28,7 +29,11 @@ namespace ws {
 template <typename T>
 WS_HD inline T repeat_add(T x, T c, int n) {
     constexpr int kDigits = sizeof(T) == 4 ? 24 : 53;                 // significand bits
-    constexpr int64_t kTop = (int64_t)1 << kDigits;                    // 2^e / u
+    // integer arithmetic in units of the ulp: every quantity is below 2^(kDigits + 1), so
+    // fp32 runs it in 32-bit integers (single conversions and a 32-bit division on the GPU,
+    // where 64-bit ones are long software sequences)
+    using I = std::conditional_t<sizeof(T) == 4, int32_t, int64_t>;
+    constexpr I kTop = (I)1 << kDigits;                                // 2^e / u
     const T kMinBulk = sizeof(T) == 4 ? T(1e-30) : T(1e-290);          // well inside the normal range
     while (n > 0) {
         const T y = x + c;  // one real step
@@ -36,22 +41,23 @@ WS_HD inline T repeat_add(T x, T c, int n) {
         x = y;
         if (n == 0 || !(y >= kMinBulk) || !(c > T(0)) || !std::isfinite(y)) continue;
         int e = 0;
-        (void)std::frexp(y, &e);                        // y in [2^(e-1), 2^e)
-        const T u = std::ldexp(T(1), e - kDigits);      // its ulp
-        const T q = c / u;                              // exact: u is a power of two
+        (void)std::frexp(y, &e);                        // y in [2^(e-1), 2^e), ulp u = 2^(e - kDigits)
+        // scalings by powers of two (exact; no divisions: the device pass runs this per value)
+        const T q = std::ldexp(c, kDigits - e);         // c / u
         if (!(q < T(kTop))) continue;                   // c spans the binade: single steps
         const T qf = std::floor(q);
         const T fr = q - qf;
         if (fr == T(0.5)) continue;                     // a tie: the parity decides, single steps
-        const int64_t D = (int64_t)qf + (fr > T(0.5) ? 1 : 0);   // increment in units of u
+        const I D = (I)qf + (fr > T(0.5) ? 1 : 0);      // increment in units of u
         if (D == 0) return y;                           // c rounds away: y never moves again
-        const int64_t Y = (int64_t)(y / u);             // exact integer < 2^kDigits
-        const int64_t Cc = (int64_t)std::ceil(q);
+        const I Y = (I)std::ldexp(y, kDigits - e);      // y / u: an integer < 2^kDigits
+        const I Cc = (I)std::ceil(q);
         // bulk steps j = 0 .. m-1 from z_j = y + j d need z_j + c <= 2^e - u
-        const int64_t room = kTop - 1 - Y - Cc;
+        const I room = kTop - 1 - Y - Cc;
         if (room < 0) continue;
-        const int64_t m = room / D + 1 < (int64_t)n ? room / D + 1 : (int64_t)n;
-        x = T(Y + m * D) * u;                           // exact: a multiple of u below 2^e
+        const I steps = room / D + 1;
+        const I m = steps < (I)n ? steps : (I)n;
+        x = std::ldexp(T(Y + m * D), e - kDigits);      // exact: a multiple of u below 2^e
         n -= (int)m;
     }
     return x;

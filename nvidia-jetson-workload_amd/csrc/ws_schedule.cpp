@@ -629,7 +629,8 @@ void run_steps(ws_sim* s, int k) {
     // PE: T / P updates on the aux stream, in step order there, concurrent with the stencil
     // kernels (they touch neither u, v, h nor each other's inputs across streams); the aux
     // stream starts after everything queued so far and the main stream waits for it at the end
-    s->aux_active = k > 0 && s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS;
+    const bool pe_run = k > 0 && s->cfg.model == WS_MODEL_PRIMITIVE_EQUATIONS;
+    s->aux_active = pe_run;
     if (s->aux_active) {
         if (!s->aux) {
             WS_HIP_CHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
@@ -638,6 +639,8 @@ void run_steps(ws_sim* s, int k) {
         }
         WS_HIP_CHECK(hipEventRecord(s->aux_in, s->stream));
         WS_HIP_CHECK(hipStreamWaitEvent(s->aux, s->aux_in, 0));
+    }
+    if (pe_run) {
         // the T / P drift of the whole run in one pass at its end (tp_flush; on a throw, the
         // guard below applies the completed launches' drift before the error leaves run())
         s->tp_lazy = true;
