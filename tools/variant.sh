@@ -9,7 +9,7 @@ make -s -j8 >/dev/null
 NAME=$1; DEFS=${2:-}; SRCS=${3:-ws_fused_dppy_f64_2.hip}  # one or more sources, space separated
 mkdir -p _obj/var ../lib/variants
 FLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../../include -I/opt/rocm/include"
-OBJS=$(ls _obj/*.o)
+OBJS=$(ls _obj/*.hip.o _obj/*.cpp.o)  # (not -save-temps' per-target intermediates)
 VOBJS=""
 for SRC in $SRCS; do
   /opt/rocm/bin/hipcc $FLAGS $DEFS -c $SRC -o _obj/var/${NAME}_$SRC.o
