@@ -325,15 +325,16 @@ def bvort_words_per_cell(method, W, H):
     return sum(fft + s for s in stencil)
 
 
-def bench_bvort(args, conf, method, world):
-    """Physics-mode barotropic (config c3p): one process, the whole model on one GPU."""
+def bench_bvort(args, conf, method, world, rank=0, local=0, dist=None):
+    """Physics-mode barotropic (config c3p): one GPU; `--slabs N` N slabs of the ring
+    decomposition on this GPU (one process: block transposes and halos by device copies);
+    world > 1 one rank per GPU (ws_bvort_create_slab: RCCL block all-to-all + ring halos;
+    strong scaling of the global grid)."""
     import numpy as np
     import torch
     import weather_sim as ws
     from oracle import bvort_oracle as bo
 
-    if world > 1:
-        raise SystemExit("c3p runs on one GPU (the spectral Poisson solve is not slab-decomposed)")
     W, H = conf["W"], conf["H"]
     cfg = ws.SimulationConfig()
     cfg.grid_width, cfg.grid_height = W, H
@@ -342,41 +343,59 @@ def bench_bvort(args, conf, method, world):
     # beta small enough that the gravest Rossby mode (omega ~ beta W / 2 pi) stays inside
     # RK4's stability region at this dt
     cfg.dt, cfg.beta, cfg.viscosity = 0.05, 1e-3, 0.01
-    m = ws.BarotropicVorticityModel(cfg)
+    cfg.device_id = local
+    if world > 1:
+        m = ws.BarotropicVorticityModel(cfg, slab=(rank, world, bootstrap_uid(dist, rank, ws.new_comm_id)))
+        parallelism = f"y-slabs over {world} GPUs (RCCL block transposes + ring halos)"
+    elif args.slabs > 1:
+        m = ws.BarotropicVorticityModel(cfg, devices=[local] * args.slabs)
+        parallelism = f"{args.slabs} y-slabs on one GPU (one process, device-copy transposes and halos)"
+    else:
+        m = ws.BarotropicVorticityModel(cfg)
+        parallelism = "single GPU"
     z0 = bo.rossby_mode(W, H, 1.0, 1.0, 5, 3, amp=1e-2) + bo.rossby_mode(W, H, 1.0, 1.0, 2, 7, amp=5e-3)
-    m.set_vorticity(z0)
+    m.set_vorticity(z0[m.row0:m.row0 + m.rows])  # a rank's slab: its own rows
     if args.warmup > 0:
         m.run(args.warmup)
-    clock_ramp(lambda: m.run(2) or 2, None, args.warmup > 0)  # one GPU (world 1), as in main()
+    clock_ramp(lambda: m.run(2) or 2, dist if world > 1 else None, args.warmup > 0)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     m.run(args.steps)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(dist, elapsed)
     dev_ms, launches = m.last_run_stats()
     if not np.isfinite(m.get_vorticity_field()).all():
         raise SystemExit("c3p: vorticity is not finite after the timed run")
+    if rank != 0:
+        return
     w = 8 if conf["fp64"] else 4
-    step_bytes = bvort_words_per_cell(method, W, H) * w * W * H
+    step_bytes = bvort_words_per_cell(method, W, H) * w * W * m.rows  # this rank's (or the whole) grid
     step_ms = dev_ms / args.steps
     achieved = step_bytes / (step_ms * 1e-3) / 1e9
     result = {
-        "metric": METRIC, "value": W * H * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": 1,
+        "metric": METRIC, "value": W * H * args.steps / elapsed, "unit": "cell-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "f64" if conf["fp64"] else "f32",
         "data": "synthetic (two Rossby modes), inputs resident in HBM",
         "config": {"workload": conf["workload"] + f", {args.method.upper()}", "grid": [W, H], "levels": 1,
-                   "integrator": args.method, "parallelism": "single GPU"},
+                   "integrator": args.method, "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": _step_traffic(args, launches / args.steps),
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": _step_traffic(args, launches / args.steps) if parallelism == "single GPU" else None,
                      "kernel": "whole step (LDS-FFT Poisson: bv_rowfft_fwd + bv_colsolve + bv_rowfft_inv, then bv_stage_kernel)",
                      "bytes_per_launch": step_bytes, "mean_launch_ms": step_ms,
                      "note": "device time of the run (hipEvents on the model's stream) per step; "
                              "bytes = bvort_words_per_cell x cells"},
         "launches_per_step": launches / args.steps,
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         # the NumPy oracle (a port: no reference exists for this model), bounded sample
         z = z0.astype(np.float64)
         t0 = time.perf_counter()
@@ -555,8 +574,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--method", default="rk4", choices=sorted(METHODS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--slabs", type=int, default=1, help="c4p: N y-slabs of the ring decomposition on this GPU "
-                                                          "(one process; measures the decomposition's cost)")
+    ap.add_argument("--slabs", type=int, default=1, help="c3p / c4p: N y-slabs of the ring decomposition on this "
+                                                          "GPU (one process; measures the decomposition's cost)")
     ap.add_argument("--no-check", action="store_true", help="skip the parity self-check (profiling runs)")
     ap.add_argument("--pin", default=None, help="kernel:steps_per_launch:seg_rows:align (profiling runs pin "
                                                 "the variant a bench run chose)")
@@ -586,7 +605,7 @@ def main():
     conf = CONFIGS[args.config]
     method = METHODS[args.method]
     if args.config == "c3p":
-        return bench_bvort(args, conf, method, world)
+        return bench_bvort(args, conf, method, world, rank, local, dist)
     if args.config == "c4p":
         return bench_lpe(args, conf, method, world, rank, local, dist)
     cfg = ws.SimulationConfig()

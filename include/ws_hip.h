@@ -332,6 +332,24 @@ int ws_bvort_get_field(ws_bvort_t* model, int32_t which, void* host, int32_t hei
 int ws_bvort_run(ws_bvort_t* model, int32_t num_steps);
 int ws_bvort_get_state(const ws_bvort_t* model, double* time, int32_t* step, double* last_run_ms,
                        int64_t* last_run_launches);
+/* y-slab decomposition of the vorticity model around its periodic ring (new; LDS-FFT Poisson
+ * path only: power-of-two width and height, a power-of-two slab count n with height % (2 n) ==
+ * 0 and (width / 2) % n == 0). The row FFTs stay local to a slab; the spectrum is transposed
+ * in blocks of width / (2 n) columns to the column pass and back (slab q solves global columns
+ * [q nc, (q + 1) nc)), and the stencil reads one halo row of psi and zeta from the ring
+ * neighbours. Every pass is the single domain's on the same rows / columns: results are
+ * bitwise identical to ws_bvort_create's. ws_bvort_create_multi: ONE model over `ndevices`
+ * slabs in this process, slab r on devices[r] (repeats share a device; transposes and halos by
+ * the process's own copies); used like ws_bvort_create's (whole fields in and out). */
+int ws_bvort_create_multi(const ws_config_t* cfg, int32_t poisson, const int32_t* devices, int32_t ndevices,
+                          ws_bvort_t** out);
+/* One rank of a process-per-GPU decomposition (device cfg->device_id): transposes by RCCL
+ * send / receive per block, halos by the periodic plan of ws_lpe_exchange_plan's kind; set /
+ * get take the rank's rows (height = rows); run() and field reads that need psi are
+ * collective. */
+int ws_bvort_create_slab(const ws_config_t* cfg, int32_t poisson, int32_t rank, int32_t nranks,
+                         const uint8_t id[WS_COMM_ID_BYTES], ws_bvort_t** out, int32_t* row0, int32_t* rows);
+int ws_bvort_layout(const ws_bvort_t* model, int32_t* nslabs, int32_t* row0, int32_t* rows);
 
 /* ---- physics-mode layered primitive-equation model (new) ----------- */
 /* BASELINE config C4 names a 3-D primitive-equation stencil with vertical columns; the

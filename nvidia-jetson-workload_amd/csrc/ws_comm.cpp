@@ -80,6 +80,24 @@ void SlabComm::exchange(void* const* fields, int nfields, int elem_size, const G
         if (plan.has[side]) hcheck(halo_unpack(plan, hf, side, staging_.recv[side], stream), "halo_unpack");
 }
 
+void SlabComm::alltoall(const std::vector<Block>& send, const std::vector<Block>& recv, hipStream_t stream) {
+    const ncclComm_t c = (ncclComm_t)comm_;
+    for (const Block& s : send)
+        if (s.peer == rank_)
+            for (const Block& r : recv)
+                if (r.peer == rank_) {
+                    if (r.bytes != s.bytes) throw CommError("alltoall: own block sizes differ");
+                    hcheck(hipMemcpyAsync(r.ptr, s.ptr, s.bytes, hipMemcpyDeviceToDevice, stream), "hipMemcpyAsync");
+                }
+    if (nranks_ == 1) return;
+    check(ncclGroupStart(), "ncclGroupStart");
+    for (const Block& s : send)
+        if (s.peer != rank_) check(ncclSend(s.ptr, s.bytes, ncclChar, s.peer, c, stream), "ncclSend");
+    for (const Block& r : recv)
+        if (r.peer != rank_) check(ncclRecv(r.ptr, r.bytes, ncclChar, r.peer, c, stream), "ncclRecv");
+    check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void SlabComm::broadcast_i32(int32_t* v, int n, int root, hipStream_t stream) {
     if (nranks_ == 1 || n <= 0) return;
     if (n > 16) throw CommError("broadcast_i32: at most 16 values");

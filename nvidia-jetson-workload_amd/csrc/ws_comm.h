@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <stdexcept>
+#include <vector>
 
 #include "ws_halo.h"
 #include "ws_internal.h"
@@ -40,6 +41,15 @@ public:
     // periodic: the ring closes (rank 0 <-> rank n-1; make_halo_plan), always packed.
     void exchange(void* const* fields, int nfields, int elem_size, const Geom& g, int depth, hipStream_t stream,
                   bool periodic = false);
+    // Block all-to-all (the vorticity model's spectrum transposes): send[i] goes to rank
+    // send[i].peer, recv[i] arrives from rank recv[i].peer -- one block per peer and direction,
+    // so the pairs match whatever the posting order; this rank's own block is a device copy.
+    struct Block {
+        void* ptr;
+        size_t bytes;
+        int peer;
+    };
+    void alltoall(const std::vector<Block>& send, const std::vector<Block>& recv, hipStream_t stream);
     // rank `root`'s n int32 values to every rank (host in, host out; synchronises `stream`)
     void broadcast_i32(int32_t* v, int n, int root, hipStream_t stream);
     // In-place max over ranks of one double (device scratch owned by the comm).

@@ -152,6 +152,9 @@ SIGNATURES = {
     "ws_bvort_get_field": [_P, _I, _P, _I, _I, _I],
     "ws_bvort_run": [_P, _I],
     "ws_bvort_get_state": [_P, _PD, _PI, _PD, _PL],
+    "ws_bvort_create_multi": [ctypes.POINTER(ws_config_t), _I, _PI, _I, _PP],
+    "ws_bvort_create_slab": [ctypes.POINTER(ws_config_t), _I, _I, _I, ctypes.POINTER(ctypes.c_uint8), _PP, _PI, _PI],
+    "ws_bvort_layout": [_P, _PI, _PI, _PI],
     "ws_lpe_create": [ctypes.POINTER(ws_config_t), _D, _PP],
     "ws_lpe_destroy": [_P],
     "ws_lpe_set_field": [_P, _I, _P, _I, _I, _I, _I],

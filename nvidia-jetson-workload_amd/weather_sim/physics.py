@@ -33,20 +33,52 @@ class BarotropicVorticityModel:
 
     _POISSON = {"auto": 0, "hipfft": 1}
 
-    def __init__(self, config, poisson="auto"):
+    def __init__(self, config, poisson="auto", devices=None, slab=None):
         """poisson: "auto" (LDS-resident FFT passes on power-of-two grids up to 4096, hipFFT
-        otherwise) or "hipfft" (hipFFT's 2-D plans always; ws_hip.h ws_bvort_create_poisson)."""
+        otherwise) or "hipfft" (hipFFT's 2-D plans always; ws_hip.h ws_bvort_create_poisson).
+
+        Slab decomposition (power-of-two grids; bitwise equal to one domain): `devices=[...]`
+        (or `config.devices` with more than one entry) -- one model over len(devices) slabs in
+        this process, whole fields in and out; `slab=(rank, nranks, comm_id)` -- one rank of a
+        process-per-GPU decomposition over RCCL, fields of the rank's rows [row0, row0 + rows).
+        """
+        from ._native import COMM_ID_BYTES
         from .weather_simulation import SimulationConfig
         if not isinstance(config, SimulationConfig):
             raise TypeError("BarotropicVorticityModel expects a SimulationConfig")
         if poisson not in self._POISSON:
             raise ValueError(f"poisson must be one of {sorted(self._POISSON)}")
+        if devices is None and slab is None and len(getattr(config, "devices", None) or ()) > 1:
+            devices = config.devices
+        if devices is not None and slab is not None:
+            raise ValueError("devices= and slab= are exclusive")
         self._cfg = config
         raw = config._to_c()
         h = ctypes.c_void_p()
-        check(lib.ws_bvort_create_poisson(ctypes.byref(raw), self._POISSON[poisson], ctypes.byref(h)))
+        mode = self._POISSON[poisson]
+        if slab is not None:
+            rank, nranks, comm_id = slab
+            if comm_id is None or len(comm_id) != COMM_ID_BYTES:
+                raise ValueError(f"comm_id must be {COMM_ID_BYTES} bytes (weather_sim.new_comm_id())")
+            idb = (ctypes.c_uint8 * COMM_ID_BYTES)(*comm_id)
+            r0, nr = ctypes.c_int32(), ctypes.c_int32()
+            check(lib.ws_bvort_create_slab(ctypes.byref(raw), mode, int(rank), int(nranks), idb, ctypes.byref(h),
+                                           ctypes.byref(r0), ctypes.byref(nr)))
+        elif devices is not None:
+            devs = [int(d) for d in devices]
+            if not devs:
+                raise ValueError("devices must name at least one device")
+            arr = (ctypes.c_int32 * len(devs))(*devs)
+            check(lib.ws_bvort_create_multi(ctypes.byref(raw), mode, arr, len(devs), ctypes.byref(h)))
+        else:
+            check(lib.ws_bvort_create_poisson(ctypes.byref(raw), mode, ctypes.byref(h)))
         self._h = h
-        self.width, self.height = int(config.grid_width), int(config.grid_height)
+        ns, r0, nr = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib.ws_bvort_layout(self._h, ctypes.byref(ns), ctypes.byref(r0), ctypes.byref(nr)))
+        self.nslabs, self.row0, self.rows = ns.value, r0.value, nr.value
+        # a process's slab holds its own rows only
+        self.width, self.height = int(config.grid_width), self.rows
+        self.global_height = int(config.grid_height)
         self.dtype = np.float64 if config.double_precision else np.float32
 
     def __del__(self):

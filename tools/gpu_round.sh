@@ -13,6 +13,7 @@
 #   prof_default          rocprofv3 --kernel-trace --stats of the default bench command itself
 #   pin:CFG:PINS          tools/pin_timing.py (ms/step of pinned variants, one process)
 #   lpeslabs[:LIST]       c4p bench lines at N slabs of the ring decomposition on this GPU (default 1,2,8)
+#   bvslabs[:LIST]        the same for c3p (the vorticity model's decomposition)
 #
 # Every step runs under its own time limit; the first failing step ends the script (a GPU
 # fault, abort or time limit must not be followed by more GPU work in the same call).
@@ -73,13 +74,14 @@ print('%-9s %-5s %8.2f Gcell/s %8.4f ms/step %s tb %s seg %s launch %.4f ms frac
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run \
           --output-format csv -- python3 "$R/bench.py" > "$OUT/prof_default/bench.json" 2> "$OUT/prof_default/bench.err")
       rc=$?; cut -c1-200 "$OUT/prof_default/bench.json"; [ $rc -eq 0 ] || fail "$step" $rc ;;
-    lpeslabs)
-      mkdir -p "$OUT/c4p"
+    lpeslabs|bvslabs)
+      c=$([ "$name" = lpeslabs ] && echo c4p || echo c3p)
+      mkdir -p "$OUT/$c"
       for n in $(echo "${rest:-1,2,8}" | tr ',' ' '); do
-        timeout -k 10 300 python bench.py --config c4p --slabs $n --steps 100 --warmup 20 --no-cpu-baseline \
-            > "$OUT/c4p/slabs$n.json" 2> "$OUT/c4p/slabs$n.err"
-        rc=$?; [ $rc -eq 0 ] || { tail -3 "$OUT/c4p/slabs$n.err"; fail "$step (slabs $n)" $rc; }
-        python3 -c "import json; d=json.load(open('$OUT/c4p/slabs$n.json')); print('$n', d['value']/1e9, d['ms_per_step'], d['config']['parallelism'])"
+        timeout -k 10 300 python bench.py --config $c --slabs $n --steps 100 --warmup 20 --no-cpu-baseline \
+            > "$OUT/$c/slabs$n.json" 2> "$OUT/$c/slabs$n.err"
+        rc=$?; [ $rc -eq 0 ] || { tail -3 "$OUT/$c/slabs$n.err"; fail "$step (slabs $n)" $rc; }
+        python3 -c "import json; d=json.load(open('$OUT/$c/slabs$n.json')); print('$c', '$n', d['value']/1e9, d['ms_per_step'], d['config']['parallelism'])"
       done ;;
     *)
       echo "unknown step '$step'"; exit 2 ;;
