@@ -54,7 +54,7 @@ for pin in args.pins.split(","):
     sim.run(600)  # clocks up
     sim.synchronize()
     _native.check(lib.ws_diag_wave_stamps_reset())
-    sim.run(2)    # the launch recorded
+    sim.run(int(tb))  # the launch recorded (one launch of steps_per_launch steps)
     sim.synchronize()
     buf = np.zeros(MAXW * WORDS, dtype=np.uint64)
     _native.check(lib.ws_diag_wave_stamps(buf.ctypes.data, buf.nbytes))
