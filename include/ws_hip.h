@@ -464,13 +464,19 @@ int ws_sim_steps_per_launch(const ws_sim_t* sim, int32_t* steps);
  * than the edge bands' measured cost (needs >= 3 x block x NST rows per slab); a slab group
  * (one process) overlaps whenever there is an interior. WS_SLAB_OVERLAP=0|1 fixes it.
  * ws_sim_set_slab_schedule: block (> 0; <= 0 keeps it; every rank must pass the same values)
- * and overlap mode; ws_sim_slab_exchange_us: the measured exchange (auto mode; -1 if none). */
+ * and overlap mode; ws_sim_slab_exchange_us: the measured exchange (auto mode; -1 if none);
+ * ws_sim_slab_trial_ms: the auto schedule's trial, ms per block period of each schedule
+ * (ms[0] stream-ordered, ms[1] overlapped; max over ranks; -1 until a trial ran). The trial
+ * keeps the overlap iff ms[1] < ms[0] * (1 - WS_OVERLAP_MARGIN): on a near-tie the
+ * stream-ordered schedule (no cross-stream waits) stays. */
+#define WS_OVERLAP_MARGIN 0.02
 #define WS_OVERLAP_OFF 0
 #define WS_OVERLAP_ON 1
 #define WS_OVERLAP_AUTO 2
 int ws_sim_slab_schedule(const ws_sim_t* sim, int32_t* block, int32_t* overlap);
 int ws_sim_set_slab_schedule(ws_sim_t* sim, int32_t block, int32_t overlap);
 int ws_sim_slab_exchange_us(const ws_sim_t* sim, double* us);
+int ws_sim_slab_trial_ms(const ws_sim_t* sim, double* ms);
 
 /* CFL number of the current state (new: the reference's dt is fixed and it has no CFL):
  * max over cells of max((|u| + sqrt(g h)) dt / dx, (|v| + sqrt(g h)) dt / dy), computed in

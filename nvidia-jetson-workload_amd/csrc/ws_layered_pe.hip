@@ -563,14 +563,14 @@ ws_lpe* lpe_make(const ws_config_t* cfg, double gp, int device, int rank, int nr
 bool enable_peer(int dev, int peer) {
     if (dev == peer) return true;
     int ok = 0;
-    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) return false;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) {
+        (void)hipGetLastError();  // (no sticky error for the next launch check to report)
+        return false;
+    }
     hck(hipSetDevice(dev), "hipSetDevice");
     const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
-    if (e == hipErrorPeerAccessAlreadyEnabled) {
-        (void)hipGetLastError();
-        return true;
-    }
-    return e == hipSuccess;
+    if (e != hipSuccess) (void)hipGetLastError();  // already enabled, or the runtime's copies instead
+    return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
 }
 
 }  // namespace

@@ -158,6 +158,12 @@ int ws_multi_create(const ws_config_t* cfg, const int32_t* devices, int32_t ndev
             *out = mu;
             return;
         }
+        // every device is made current once on the caller's thread first: a rank whose device
+        // fails on its worker thread would return before joining the communicator, and the
+        // other ranks would wait in ncclCommInitRank for it forever. (What create_slab checks
+        // before the join -- rank, rows, config -- is the same on every rank, so it fails on
+        // all of them alike; after the join a failing rank cannot block the others.)
+        for (int r = 0; r < ndevices; ++r) set_device(devices[r]);
         try {
             uint8_t id[WS_COMM_ID_BYTES];
             set_device(devices[0]);

@@ -650,18 +650,27 @@ void run_steps(ws_sim* s, int k) {
     }
     // A run that throws after some launches (a HIP / RCCL error) must not leave the T / P drift
     // pending: T / P would lag u, v, h, and a later flush would overwrite fields reset or set in
-    // between. The guard flushes what the completed launches owe (normal exits flushed already).
+    // between. The guard flushes what the completed launches owe (normal exits flushed already)
+    // and, like the normal exit, joins the aux stream back into the compute stream: the flush
+    // runs on the aux stream, which ws_sim_synchronize, field reads and grid resets never wait on.
     struct TpGuard {
         ws_sim* s;
         ~TpGuard() {
-            if (!s->tp_lazy) return;
             try {
-                if (s->dtype == WS_F64) tp_flush<double>(s);
-                else tp_flush<float>(s);
+                if (s->tp_lazy) {
+                    if (s->dtype == WS_F64) tp_flush<double>(s);
+                    else tp_flush<float>(s);
+                }
             } catch (...) {
             }
             s->tp_lazy = false;
             s->tp_steps = 0;
+            if (s->aux_active) {
+                if (hipEventRecord(s->aux_out, s->aux) != hipSuccess ||
+                    hipStreamWaitEvent(s->stream, s->aux_out, 0) != hipSuccess)
+                    (void)hipStreamSynchronize(s->aux);  // (the join by events failed: drain it)
+                s->aux_active = false;
+            }
         }
     } tp_guard{s};
     // n steps from a block boundary on one schedule: stream-ordered launches, or the overlap
@@ -726,7 +735,9 @@ void run_steps(ws_sim* s, int k) {
         }
         s->trial_ms[0] = so;
         s->trial_ms[1] = ov;
-        s->overlap = ov < so;
+        // a near-tie keeps the stream-ordered schedule (no cross-stream waits): the samples of
+        // two schedules that cost the same differ by sync jitter, box to box
+        s->overlap = ov < so * (1.0 - WS_OVERLAP_MARGIN);
         s->overlap_trial = false;
         segment(k - 16 * s->block, s->overlap && overlap_active(s));
     } else {

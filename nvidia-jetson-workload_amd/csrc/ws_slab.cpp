@@ -152,6 +152,7 @@ int ws_sim_set_slab_schedule(ws_sim_t* s, int32_t block, int32_t overlap) {
         s->overlap = overlap == WS_OVERLAP_ON;
         s->xfer_us = -1.0;  // auto: measured again at the next run
         s->overlap_trial = false;
+        s->trial_ms[0] = s->trial_ms[1] = -1.0;
     });
 }
 
@@ -159,6 +160,14 @@ int ws_sim_slab_exchange_us(const ws_sim_t* s, double* us) {
     return guarded([&] {
         require(s != nullptr && us != nullptr, WS_ERR_INVALID, "null pointer");
         *us = s->xfer_us;
+    });
+}
+
+int ws_sim_slab_trial_ms(const ws_sim_t* s, double* ms) {
+    return guarded([&] {
+        require(s != nullptr && ms != nullptr, WS_ERR_INVALID, "null pointer");
+        ms[0] = s->trial_ms[0];
+        ms[1] = s->trial_ms[1];
     });
 }
 

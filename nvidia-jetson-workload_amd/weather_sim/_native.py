@@ -117,6 +117,7 @@ SIGNATURES = {
     "ws_sim_create_slab_emulated": [ctypes.POINTER(ws_config_t), _I, _I, _D, _PP, _PI, _PI],
     "ws_sim_set_slab_schedule": [_P, _I, _I],
     "ws_sim_slab_exchange_us": [_P, _PD],
+    "ws_sim_slab_trial_ms": [_P, _PD],
     "ws_sim_pin_variant": [_P, _I, _I, _I, _I],
     "ws_slab_partition": [_I, _I, _I, _PI, _PI],
     "ws_sim_comm_allreduce_max": [_P, _D, _PD],

@@ -136,7 +136,20 @@ class SimulationConfig:
         c = _native.ws_config_t()
         for name, _ in _native.ws_config_t._fields_:
             setattr(c, name, type(getattr(c, name))(getattr(self, name)))
+        c.device_id = self._single_device()
         return c
+
+    def _single_device(self):
+        """devices=[d] (one entry) names the device of a one-GPU run: it is device_id, and a
+        device_id other than the default 0 that disagrees with it is an error (a single entry
+        used to be ignored silently)."""
+        devs = list(self.devices or ())
+        if len(devs) != 1:
+            return int(self.device_id)
+        d = int(devs[0])
+        if int(self.device_id) not in (0, d):
+            raise ValueError(f"devices={devs} disagrees with device_id={self.device_id}")
+        return d
 
     @classmethod
     def _from_c(cls, c, output_path="./output"):
@@ -762,6 +775,16 @@ class WeatherSimulation:
         us = ctypes.c_double()
         check(lib.ws_sim_slab_exchange_us(self._h, ctypes.byref(us)))
         return us.value
+
+    def slab_trial_ms(self):
+        """Extension: the auto schedule's trial (ms per block period stream-ordered,
+        overlapped; max over ranks; (-1, -1) until a trial ran). The overlap is kept iff
+        overlapped < stream-ordered x (1 - OVERLAP_MARGIN) (ws_hip.h ws_sim_slab_trial_ms)."""
+        ms = (ctypes.c_double * 2)()
+        check(lib.ws_sim_slab_trial_ms(self._h, ms))
+        return ms[0], ms[1]
+
+    OVERLAP_MARGIN = 0.02  # ws_hip.h WS_OVERLAP_MARGIN
 
     def pin_variant(self, kernel=None, steps_per_launch=None, seg_rows=None, align=None):
         """Extension: fix (parts of) the fused-kernel variant the autotuner would choose

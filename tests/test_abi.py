@@ -194,3 +194,19 @@ def test_kernel_variant_ids_match_header():
     src = open(os.path.join(ROOT, "nvidia-jetson-workload_amd", "csrc", "ws_runtime.cpp")).read()
     for name in ids:
         assert f'{{"{name}", ' in src, name
+
+
+def test_single_device_list_names_the_device():
+    """config.devices with one entry is the device of a one-GPU run (it used to be
+    ignored, the run going to device_id 0); a device_id that disagrees with it is an error."""
+    c = ws.SimulationConfig()
+    assert c._to_c().device_id == 0
+    c.devices = [2]
+    assert c._to_c().device_id == 2
+    c.device_id = 2
+    assert c._to_c().device_id == 2
+    c.device_id = 1
+    with pytest.raises(ValueError):
+        c._to_c()
+    c.devices = [0, 1]  # several: the multi-GPU path, device_id untouched
+    assert c._to_c().device_id == 1

@@ -161,27 +161,39 @@ def test_emulated_slab_measurement_aid(ovl, monkeypatch):
     assert np.isfinite(sim.get_current_grid()._get("h")).all()
 
 
-@pytest.mark.parametrize("xfer_us,expect", [(0.0, False), (150.0, True)])
-def test_auto_schedule_from_measured_trial(xfer_us, expect, monkeypatch):
+@pytest.mark.parametrize("xfer_us", [0.0, 150.0])
+def test_auto_schedule_from_measured_trial(xfer_us, monkeypatch):
     """WS_OVERLAP_AUTO (the multi-GPU default): the first run times the block's halo exchange
     (reported); the first run of at least sixteen blocks then alternates four-block segments of
-    each schedule, times their last three blocks and keeps the faster (ws_schedule.cpp run_steps). On the emulated slab the
-    exchange is a timed wait of xfer_us: none -> the overlap's extra edge launches lose; 150 us
-    -> hiding the wait behind the interior wins."""
+    each schedule, times their last three blocks and keeps the faster (ws_schedule.cpp
+    run_steps), the stream-ordered one on a near-tie (WS_OVERLAP_MARGIN).
+
+    Which schedule wins is a property of the box, not of the code (round 5: a 150 us wait on
+    a 100-row slab picked stream-ordered on one box and overlap on four others), so the test
+    asserts only what is deterministic: the decision follows the reported trial times, the
+    stream-ordered period contains the emulated wait (it is on the compute stream), and both
+    schedules keep the run finite and the caller's override wins."""
     monkeypatch.delenv("WS_SLAB_OVERLAP", raising=False)
     sim = ws.WeatherSimulation(_cfg(256, 4 * 100, 2, True), _slab=(1, 4, None, xfer_us))
     assert sim.slab_exchange_us() == -1.0 and sim.slab_schedule() == (6, False)  # not measured yet
+    assert sim.slab_trial_ms() == (-1.0, -1.0)
     sim.set_initial_condition(ws.JetStreamInitialCondition())
     sim.initialize()
     assert sim.run(7) == 7  # fewer than sixteen blocks: the exchange is timed, the trial waits
     us = sim.slab_exchange_us()
     assert us >= xfer_us * 0.9 and us < xfer_us + 1000.0
-    assert sim.slab_schedule() == (6, False)
-    assert sim.run(100) == 100  # the trial (sixteen blocks), then the faster schedule
-    assert sim.slab_schedule() == (6, expect)
+    assert sim.slab_schedule() == (6, False) and sim.slab_trial_ms() == (-1.0, -1.0)
+    assert sim.run(100) == 100  # the trial (sixteen blocks), then the chosen schedule
+    so, ov = sim.slab_trial_ms()
+    msg = f"trial: stream-ordered {so:.4f} ms / block, overlapped {ov:.4f} ms / block, wait {xfer_us} us"
+    print(msg)
+    assert so > 0 and ov > 0, msg
+    assert so >= 0.9 * xfer_us * 1e-3, msg  # the stream-ordered block waits for the exchange
+    assert sim.slab_schedule() == (6, ov < so * (1.0 - sim.OVERLAP_MARGIN)), msg
     assert np.isfinite(sim.get_current_grid()._get("h")).all()
     sim.set_slab_schedule(3, "off")  # fixed by the caller from now on
     assert sim.slab_schedule() == (3, False) and sim.slab_exchange_us() == -1.0
+    assert sim.slab_trial_ms() == (-1.0, -1.0)
     assert sim.run(4) == 4
     with pytest.raises(ValueError):
         sim.set_slab_schedule(7, "on")  # 7 x 4 rows > the 24 halo rows
