@@ -103,14 +103,17 @@ __device__ __forceinline__ VT fmadd(VT a, VT b, VT c) {
     return __builtin_elementwise_fma(a, b, c);
 }
 
+// the tendency from the cell (c), its x-derivatives X = (u_x, v_x, h_x) (cdiff of its right
+// and left neighbours) and its top / bottom neighbours: the x-derivatives depend only on the
+// cell's row, so a march may form them ahead of the rest (ws_fused_dppy_kernel.h)
 template <int MODE, typename VT, typename T>
-__device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V3<VT>& r, const V3<VT>& t,
-                                       const V3<VT>& b, const Spacing<T>& sp, T g, T f) {
-    const VT u_x = cdiff<MODE>(r.u, l.u, sp.two_dx, sp.inv2dx);
+__device__ __forceinline__ V3<VT> tend_x(const V3<VT>& c, const V3<VT>& X, const V3<VT>& t, const V3<VT>& b,
+                                         const Spacing<T>& sp, T g, T f) {
+    const VT u_x = X.u;
     const VT u_y = cdiff<MODE>(b.u, t.u, sp.two_dy, sp.inv2dy);
-    const VT v_x = cdiff<MODE>(r.v, l.v, sp.two_dx, sp.inv2dx);
+    const VT v_x = X.v;
     const VT v_y = cdiff<MODE>(b.v, t.v, sp.two_dy, sp.inv2dy);
-    const VT h_x = cdiff<MODE>(r.h, l.h, sp.two_dx, sp.inv2dx);
+    const VT h_x = X.h;
     const VT h_y = cdiff<MODE>(b.h, t.h, sp.two_dy, sp.inv2dy);
     V3<VT> k;
     if constexpr (MODE >= kSpFast) {
@@ -130,6 +133,19 @@ __device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V
         k.h = -c.h * (u_x + v_y) - c.u * h_x - c.v * h_y;
     }
     return k;
+}
+
+// x-derivatives (u_x, v_x, h_x) from the left / right neighbours
+template <int MODE, typename VT, typename T>
+__device__ __forceinline__ V3<VT> xdiffs(const V3<VT>& l, const V3<VT>& r, const Spacing<T>& sp) {
+    return V3<VT>{cdiff<MODE>(r.u, l.u, sp.two_dx, sp.inv2dx), cdiff<MODE>(r.v, l.v, sp.two_dx, sp.inv2dx),
+                  cdiff<MODE>(r.h, l.h, sp.two_dx, sp.inv2dx)};
+}
+
+template <int MODE, typename VT, typename T>
+__device__ __forceinline__ V3<VT> tend(const V3<VT>& c, const V3<VT>& l, const V3<VT>& r, const V3<VT>& t,
+                                       const V3<VT>& b, const Spacing<T>& sp, T g, T f) {
+    return tend_x<MODE>(c, xdiffs<MODE>(l, r, sp), t, b, sp, g, f);
 }
 
 // stage update y + c k (fast numerics: one fused multiply-add)

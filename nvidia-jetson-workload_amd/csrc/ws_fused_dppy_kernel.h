@@ -56,15 +56,12 @@ struct XEdge {
     bool lo, hi, hi1;
 };
 
-// One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage.
-// XCLAMP / YCLAMP: the strip / segment touches a global edge, where the reference clamps
-// the neighbour index to the cell itself (weather_simulation.cpp:510-513).
-// l / r: the mid row's left / right neighbours (DPP lane shifts, or LDS reads: see
-// kLdsStages below). VT = T, or P2<T> for a column pair (element-wise).
-template <int MODE, bool XCLAMP, bool YCLAMP, typename VT, typename T>
-__device__ __forceinline__ V3<VT> stage_tend_lr(const XEdge& e, int j, const Geom& g, const V3<VT>& up,
-                                                const V3<VT>& mid, const V3<VT>& down, V3<VT> l, V3<VT> r,
-                                                const Spacing<T>& sp, T grav, T cor) {
+// A stage's x-derivatives (u_x, v_x, h_x) of its mid row from the mid row's left / right
+// neighbours l / r (DPP lane shifts, or LDS reads: see kLdsStages below). XCLAMP: the strip
+// touches a global x edge, where the reference clamps the neighbour index to the cell itself
+// (weather_simulation.cpp:510-513). VT = T, or P2<T> for a column pair (element-wise).
+template <int MODE, bool XCLAMP, typename VT, typename T>
+__device__ __forceinline__ V3<VT> stage_x(const XEdge& e, const V3<VT>& mid, V3<VT> l, V3<VT> r, const Spacing<T>& sp) {
     if constexpr (XCLAMP) {
         if constexpr (std::is_same_v<VT, T>) {
             l = V3<VT>{e.lo ? mid.u : l.u, e.lo ? mid.v : l.v, e.lo ? mid.h : l.h};
@@ -76,14 +73,23 @@ __device__ __forceinline__ V3<VT> stage_tend_lr(const XEdge& e, int j, const Geo
             if (e.hi1) { r.u.y = mid.u.y; r.v.y = mid.v.y; r.h.y = mid.h.y; }
         }
     }
+    return xdiffs<MODE>(l, r, sp);
+}
+
+// One stage at row j from rows j-1 (up), j (mid), j+1 (down) of the previous stage and the mid
+// row's x-derivatives X (stage_x). YCLAMP: the segment touches a global y edge (clamp-to-self).
+template <int MODE, bool YCLAMP, typename VT, typename T>
+__device__ __forceinline__ V3<VT> stage_tend_x(int j, const Geom& g, const V3<VT>& up, const V3<VT>& mid,
+                                               const V3<VT>& down, const V3<VT>& X, const Spacing<T>& sp, T grav,
+                                               T cor) {
     if constexpr (YCLAMP) {
         const bool ytop = (j == 0) && g.top_clamp;
         const bool ybot = (j == g.H - 1) && g.bot_clamp;
         const V3<VT> t = ytop ? mid : up;
         const V3<VT> b = ybot ? mid : down;
-        return tend<MODE>(mid, l, r, t, b, sp, grav, cor);
+        return tend_x<MODE>(mid, X, t, b, sp, grav, cor);
     } else {
-        return tend<MODE>(mid, l, r, up, down, sp, grav, cor);
+        return tend_x<MODE>(mid, X, up, down, sp, grav, cor);
     }
 }
 
@@ -349,6 +355,13 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         }
     };
 
+    // stage gs's x-derivatives of its mid row (neighbours by nbrs)
+    auto xderiv = [&](auto Pc, auto GSc, auto Xc, const V3<VT>& mid, int rs, const Spacing<T>& sp) __attribute__((always_inline)) -> V3<VT> {
+        V3<VT> l, r;
+        nbrs(Pc, GSc, mid, rs, l, r);
+        return stage_x<MODE, decltype(Xc)::value>(xe, mid, l, r, sp);
+    };
+
     const V3<VT> Z{VT{}, VT{}, VT{}};
     StepRings<VT> st[NSTEP];
 #pragma unroll
@@ -357,8 +370,15 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         for (int i = 0; i < 2; ++i) st[q].Y[i] = st[q].S1[i] = st[q].S2[i] = st[q].S3[i] = st[q].K2[i] = st[q].K3[i] = st[q].O[i] = Z;
 
     const int R0 = y0 - kNS;
-    // rounded up to the unroll (SPLIT: the consumer's bodies lag kLag rows behind the march)
-    const int R1 = R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
+    // the first march row no stored output depends on: the body at row R stores row R - kNS
+    // (SPLIT: the consumer's bodies lag kLag rows behind the march). The march runs whole
+    // unrolled periods of kU bodies up to the last period that reaches it, and that period only
+    // as far as Rstop (a wave-uniform test per body): a chain of ~22 rows plus its 16 warm-up rows
+    // rounded up to whole periods ran 3.5 bodies past its cone on average
+    // (The split and fp64-pair kernels keep whole periods -- R1, rounded up: the guarded period
+    // made them spill at their register caps.)
+    constexpr bool kTail = !SPLIT && !(CPL == 2 && sizeof(T) == 8);
+    const int Rstop = kTail ? y1 + kNS : R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
 
     // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
     // stage s computes row Rq - s; the step's output row Rq - NST goes to `out`. Stage s of
@@ -367,11 +387,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // cone; whatever a body computes beyond the cone only ever reaches rows that are not
     // stored). Ring slots are indexed by the parity of the body phase P.
     auto step = [&](auto Qc, auto Pc, auto Xc, auto Yc, auto ONc, StepRings<VT>& S, const V3<VT>& i0,
-                    const V3<VT>& i1, const V3<VT>& i2, int Rq, V3<VT>& out) {
+                    const V3<VT>& i1, const V3<VT>& i2, int Rq, V3<VT>& out) __attribute__((always_inline)) {
         constexpr int q = decltype(Qc)::value;
         constexpr int P = decltype(Pc)::value;
-        constexpr bool XC = decltype(Xc)::value;
-        constexpr bool YC = decltype(Yc)::value;
+                constexpr bool YC = decltype(Yc)::value;
         constexpr auto on = [](int s) { return decltype(ONc){}(q * NST + s); };
         constexpr auto r2 = [](int d) { return ((P + d) % 2 + 2) % 2; };
         auto gsc = [](auto sc) { return std::integral_constant<int, q * NST + decltype(sc)::value>{}; };
@@ -390,36 +409,32 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
             // a temp / next grid (the config's spacing sp2; the host launches two steps at once
             // only when sp1 == sp2)
             const Spacing<T>& sp_in = q == 0 ? a.sp1 : a.sp2;
-            V3<VT> l, r;
-            nbrs(Pc, gsc(S1c{}), i1, rs1, l, r);
-            const V3<VT> k1 =
-                stage_tend_lr<MODE, XC, YC>(xe, Rq - 1, g, i2, i1, i0, l, r, sp_in, a.gravity, a.coriolis_f);
+            const V3<VT> k1 = stage_tend_x<MODE, YC>(Rq - 1, g, i2, i1, i0, xderiv(Pc, gsc(S1c{}), Xc, i1, rs1, sp_in),
+                                                     sp_in, a.gravity, a.coriolis_f);
             if constexpr (NST == 1) {
                 out = axpy<MODE>(i1, a.c_dt, k1);  // Euler: y + dt k
             } else {
                 const V3<VT> s1 = axpy<MODE>(i1, a.c_half, k1);  // y + (0.5f dt) k
                 xput(Pc, gsc(S2c{}), s1);
                 if constexpr (on(2)) {
-                    nbrs(Pc, gsc(S2c{}), S.S1[r2(-2)], 0, l, r);
-                    const V3<VT> k2 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
-                                                                 l, r, a.sp2, a.gravity, a.coriolis_f);
+                    const V3<VT> k2 = stage_tend_x<MODE, YC>(Rq - 2, g, S.S1[r2(-3)], S.S1[r2(-2)], s1,
+                                                             xderiv(Pc, gsc(S2c{}), Xc, S.S1[r2(-2)], 0, a.sp2), a.sp2,
+                                                             a.gravity, a.coriolis_f);
                     if constexpr (NST == 2) {
                         out = axpy<MODE>(i2, a.c_dt, k2);  // RK2: y + dt k2
                     } else {
                         const V3<VT> s2 = axpy<MODE>(i2, a.c_half, k2);
                         xput(Pc, gsc(S3c{}), s2);
                         if constexpr (on(3)) {
-                            nbrs(Pc, gsc(S3c{}), S.S2[r2(-3)], 0, l, r);
-                            const V3<VT> k3 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 3, g, S.S2[r2(-4)],
-                                                                         S.S2[r2(-3)], s2, l, r, a.sp2, a.gravity,
-                                                                         a.coriolis_f);
+                            const V3<VT> k3 = stage_tend_x<MODE, YC>(Rq - 3, g, S.S2[r2(-4)], S.S2[r2(-3)], s2,
+                                                                     xderiv(Pc, gsc(S3c{}), Xc, S.S2[r2(-3)], 0, a.sp2),
+                                                                     a.sp2, a.gravity, a.coriolis_f);
                             const V3<VT> s3 = axpy<MODE>(S.Y[r2(-3)], a.c_dt, k3);
                             xput(Pc, gsc(S4c{}), s3);
                             if constexpr (on(4)) {
-                                nbrs(Pc, gsc(S4c{}), S.S3[r2(-4)], 0, l, r);
-                                const V3<VT> k4 = stage_tend_lr<MODE, XC, YC>(xe, Rq - 4, g, S.S3[r2(-5)],
-                                                                             S.S3[r2(-4)], s3, l, r, a.sp2, a.gravity,
-                                                                             a.coriolis_f);
+                                const V3<VT> k4 = stage_tend_x<MODE, YC>(
+                                    Rq - 4, g, S.S3[r2(-5)], S.S3[r2(-4)], s3,
+                                    xderiv(Pc, gsc(S4c{}), Xc, S.S3[r2(-4)], 0, a.sp2), a.sp2, a.gravity, a.coriolis_f);
                                 // y + dt/6 * (((k4 + 2 k2) + 2 k3) + k4)   (k1 aliases k4, :437-451)
                                 out = rk4_final<MODE>(S.Y[r2(-4)], a.c_dt6, k4, S.K2[r2(-4)], S.K3[r2(-4)]);
                             }
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // one stored row (the last step's output, or a dropped store while it is outside the
     // cone, keeping every body's store pattern the same). KW = warm-up period index (-1 =
     // steady state): the body's march position is R - R0 = KW kU + P.
-    auto body = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+    auto body = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) __attribute__((always_inline)) {
         constexpr int P = decltype(Pc)::value;
         constexpr int KW = decltype(KWc)::value;
         struct On {
@@ -476,7 +491,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
 
     // SPLIT: the producer's body -- the first step at march row R, its output row R - NST into
     // handover slot P (no store)
-    auto pbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+    auto pbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) __attribute__((always_inline)) {
         constexpr int P = decltype(Pc)::value;
         constexpr int KW = decltype(KWc)::value;
         struct On {
@@ -498,7 +513,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // SPLIT: the consumer's body at the same phase -- march row R - kLag of the second step: its
     // input rows from the handover slots the producer filled kLag .. kLag + 2 bodies ago, its
     // output row stored
-    auto cbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) {
+    auto cbody = [&](auto Pc, auto Xc, auto Yc, auto KWc, int R) __attribute__((always_inline)) {
         constexpr int P = decltype(Pc)::value;
         constexpr int KW = decltype(KWc)::value;
         struct On {
@@ -531,28 +546,35 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
                 }(), ...);
             }(std::make_integer_sequence<int, kD>{});
         }
-        auto period = [&](auto KWc, int R) {
+        // a period of kU bodies; GUARD: only the bodies before Rstop (the march's last period)
+        auto period = [&](auto KWc, int R, auto GUARDc) __attribute__((always_inline)) {
             [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
                 ([&] {
                     constexpr int P = Ps;
+                    const bool run = !(kTail && decltype(GUARDc)::value) || R + P < Rstop;
                     if constexpr (!SPLIT) {
-                        body(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                        if (run) body(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
                     } else {
                         // both waves pass every barrier: the branch is below it
                         if constexpr (P % kLag == 0) lds_barrier();
-                        if constexpr (kProd) pbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
-                        else cbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                        if (run) {
+                            if constexpr (kProd) pbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                            else cbody(std::integral_constant<int, P>{}, Xc, Yc, KWc, R + P);
+                        }
                     }
                 }(), ...);
             }(std::make_integer_sequence<int, kU>{});
         };
-        // warm-up periods (R1 - R0 >= kU: at least the first runs), then the steady march
+        // warm-up periods (Rstop - R0 > 2 kNS: the first runs; a short march may end in one),
+        // then the steady march: whole periods, and the last one guarded
         [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
             ([&] {
-                if (Ks == 0 || R0 + Ks * kU < R1) period(std::integral_constant<int, Ks>{}, R0 + Ks * kU);
+                if (Ks == 0 || R0 + Ks * kU < Rstop) period(std::integral_constant<int, Ks>{}, R0 + Ks * kU, std::true_type{});
             }(), ...);
         }(std::make_integer_sequence<int, kNW>{});
-        for (int R = R0 + kNW * kU; R < R1; R += kU) period(std::integral_constant<int, -1>{}, R);
+        int R = R0 + kNW * kU;
+        for (; R + kU <= Rstop; R += kU) period(std::integral_constant<int, -1>{}, R, std::false_type{});
+        if (R < Rstop) period(std::integral_constant<int, -1>{}, R, std::true_type{});
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     auto march = [&](auto Xc, auto Yc) {
