@@ -43,6 +43,9 @@ struct FusedArgs {
     // seg_rows then holds the longest chain's rows.
     const ChainSeg* chains;
     int32_t nchains;
+    // wave issue priority of the launch (s_setprio; 0 = normal): an overlapped slab block's
+    // edge bands run beside its interior on the same SIMDs and are the block's critical path
+    int32_t prio;
 };
 
 // Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).

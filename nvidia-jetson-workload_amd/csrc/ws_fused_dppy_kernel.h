@@ -232,6 +232,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
 #ifdef WS_WAVE_STAMPS
     const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
 #endif
+    if (a.prio > 0) __builtin_amdgcn_s_setprio(3);  // (wave-uniform: a kernel argument)
     const int w = xcd_work_item();  // XCD-aware: neighbouring strips share an L2
     int strip, y0, y1, level;
     if (a.chains) {  // chain schedule: this workgroup's march from the host's table
@@ -375,9 +376,12 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
     // unrolled periods of kU bodies up to the last period that reaches it, and that period only
     // as far as Rstop (a wave-uniform test per body): a chain of ~22 rows plus its 16 warm-up rows
     // rounded up to whole periods ran 3.5 bodies past its cone on average
-    // (The split and fp64-pair kernels keep whole periods -- R1, rounded up: the guarded period
-    // made them spill at their register caps.)
-    constexpr bool kTail = !SPLIT && !(CPL == 2 && sizeof(T) == 8);
+    // (Only the one-column fp64 march -- C2, its slab shares -- and the fp32 pair march -- C3,
+    // C4 -- end at Rstop; the others keep whole periods, R1 rounded up: the guarded period made
+    // the split kernels spill at their register caps, and in the fp64-pair and one-column fp32
+    // instantiations the compiler merged the guarded bodies' stores into blocks that
+    // tests/test_isa_hazards.py rule 2 cannot prove address-defined.)
+    constexpr bool kTail = !SPLIT && ((CPL == 1 && sizeof(T) == 8) || (CPL == 2 && sizeof(T) == 4));
     const int Rstop = kTail ? y1 + kNS : R0 + (y1 + kNS + (SPLIT ? kLag : 0) - R0 + kU - 1) / kU * kU;
 
     // One time step's stages at march row Rq of its input (rows Rq, Rq-1, Rq-2 = i0, i1, i2):
@@ -574,7 +578,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         }(std::make_integer_sequence<int, kNW>{});
         int R = R0 + kNW * kU;
         for (; R + kU <= Rstop; R += kU) period(std::integral_constant<int, -1>{}, R, std::false_type{});
-        if (R < Rstop) period(std::integral_constant<int, -1>{}, R, std::true_type{});
+        if constexpr (kTail) {
+            if (R < Rstop) period(std::integral_constant<int, -1>{}, R, std::true_type{});
+        }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA into LDS after exit
     };
     auto march = [&](auto Xc, auto Yc) {

@@ -14,4 +14,17 @@
 #ifndef WS_DPPY_LDSX
 #define WS_DPPY_LDSX -1
 #endif
+// overlap schedule: a slab whose first launch's edge bands are at least WS_THIN_PCT % of its rows
+// runs them as latency-critical (short chains, raised priority, reserved wave slots)
+#ifndef WS_THIN_PCT
+#define WS_THIN_PCT 8
+#endif
+// shortest edge-band chain of a thin slab's overlap, in half cones (stages per launch)
+#ifndef WS_CHAIN_MIN2
+#define WS_CHAIN_MIN2 2
+#endif
+// wave issue priority of an overlapped block's edge-band launches (0: normal)
+#ifndef WS_EDGE_PRIO
+#define WS_EDGE_PRIO 1
+#endif
 // WS_WAVE_STAMPS: per-workgroup start / end / placement records (tools/wave_timeline.py)

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdio>
 
+#include "ws_knobs.h"
 #include "ws_sim.h"
 
 namespace wsr {
@@ -83,11 +84,11 @@ constexpr double kXClampCost = 1.73, kYClampCost = 1.34;
 
 template <typename T>
 static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
-                                             int out_w, int sp_mode) {
+                                             int out_w, int sp_mode, int want_chains, int min2) {
     const ws_grid* g = s->slot[0];
-    const int64_t key[10] = {nst, nsteps, A.y0, A.y1, B.y0, B.y1, rounds, out_w, s->kernel, sp_mode};
+    const int64_t key[12] = {nst, nsteps, A.y0, A.y1, B.y0, B.y1, rounds, out_w, s->kernel, sp_mode, want_chains, min2};
     for (const auto& t : s->chain_tables)
-        if (std::equal(key, key + 10, t.key)) return t;
+        if (std::equal(key, key + 12, t.key)) return t;
     if (s->num_cus == 0) {
         int cus = 0;
         WS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
@@ -97,7 +98,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     // number of waves on every SIMD whatever the kernel's occupancy (C3's launch with 1.5 waves
     // per SIMD ran half its SIMDs idle for the last 40 %, profiles/r04_timeline_c3.txt)
     const int waves_per_wg = ws::fused_split(s->kernel) ? 2 : 1;
-    const int64_t want = (int64_t)rounds * 4 * std::max(1, s->num_cus) / waves_per_wg;
+    const int64_t want = want_chains > 0 ? want_chains : (int64_t)rounds * 4 * std::max(1, s->num_cus) / waves_per_wg;
     const int cone = nst * nsteps;
     const int nstrips = (int)ws::fused_strips(s->kernel, g->W, cone, (int)elem_size(s->dtype), out_w);
     struct Group {
@@ -120,9 +121,10 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
                 groups.push_back(gr);
             }
     // chains per group in proportion to its cost (largest remainder), at least one, and none
-    // shorter than the march's warm-up (2 x the cone): a thin band -- an overlapped block's edge
-    // bands, launched beside the interior -- gets few long chains, not a chip's worth of stubs
-    const int min_rows = 2 * cone;
+    // shorter than min2 half cones (default 2 cones, the march's warm-up): a band of few rows --
+    // an overlapped block's edge bands -- gets few long chains, not a chip's worth of stubs (a
+    // thin slab's edge bands, the latency-critical path of its block, take chains of one cone)
+    const int min_rows = std::max(1, min2 * cone / 2);
     auto cap = [&](const Group& gr) { return std::max(1, gr.r.rows() / min_rows); };
     // ... and none longer than a 32-bit buffer descriptor spans (the launcher's check: rows +
     // 2 cone + 48 rows of pitch below 2^31 bytes; C5's 16384-row strips at one chain per strip)
@@ -185,7 +187,7 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     }
     // table order: chain position, then unit -- neighbouring strips at the same rows adjacent
     ws_sim::ChainTable t;
-    std::copy(key, key + 10, t.key);
+    std::copy(key, key + 12, t.key);
     std::vector<ws::ChainSeg> tab;
     for (int c = 0; c < maxn; ++c)
         for (size_t gi = 0; gi < groups.size(); ++gi)
@@ -204,14 +206,14 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
 // Launch the fused step kernel over the output rows A U B (segments of seg_rows rows, or the
 // chain schedule when seg_rows encodes one: chain_rounds).
 template <typename T>
-void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st, ws_grid* in,
-                  ws_grid* out) {
+int fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st, ws_grid* in,
+                 ws_grid* out, int want, int prio, int min2) {
     if (!st) st = s->stream;
     const int rounds = s->kernel == kKernLds ? 0 : chain_rounds(seg_rows);
     if (rounds == 0 && seg_rows <= 0) throw WsError(WS_ERR_INVALID, "bad segment rows");
     const int nA = rounds ? (A.rows() > 0) : (A.rows() + seg_rows - 1) / seg_rows;
     const int nB = rounds ? (B.rows() > 0) : (B.rows() + seg_rows - 1) / seg_rows;
-    if (nA + nB <= 0) return;
+    if (nA + nB <= 0) return 0;
     ws_grid* c = in ? in : s->slot[s->cur];    // (the autotuner times launches on other grids)
     ws_grid* n = out ? out : s->slot[1 - s->cur];
     const T dt = (T)s->dt;
@@ -227,6 +229,7 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     a.sp2 = make_spacing<T>(to_prec(s->cfg.dx, s->dtype), to_prec(s->cfg.dy, s->dtype));
     a.out_w = s->out_w(nst * nsteps);
     a.seg_rows = seg_rows;
+    a.prio = prio;
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
@@ -235,7 +238,7 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     if (s->numerics == WS_NUMERICS_FAST) ws::prepare_fast(a);
     else a.sp_mode = ws::exact_sp_mode(a);
     if (rounds) {
-        const ws_sim::ChainTable& t = chain_table<T>(s, nst, nsteps, A, B, rounds, a.out_w, a.sp_mode);
+        const ws_sim::ChainTable& t = chain_table<T>(s, nst, nsteps, A, B, rounds, a.out_w, a.sp_mode, want, min2);
         a.chains = t.dev;
         a.nchains = t.n;
         a.seg_rows = t.max_rows;  // the launcher's descriptor-span check
@@ -245,6 +248,7 @@ void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int se
     if (s->kernel == kKernLds) WS_HIP_CHECK(ws::launch_fused_step<T>(nst, a, g, st));
     else WS_HIP_CHECK(ws::launch_fused_step_dppy<T>(s->kernel, nst, nsteps, a, g, st));
     ++s->last_launches;
+    return rounds ? a.nchains : (nA + nB) * (int)s->strips(nst * nsteps) * g.L;
 }
 
 // Waves per SIMD the chosen fused variant's launches hold (hipOccupancy of the instantiation a
@@ -539,9 +543,20 @@ void overlap_edges(ws_sim* s, int steps) {
         C += n[j] * nst;
         ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[2 + j % 2];
         const BandRows r = band_rows(in, C, D);
+        // A thin slab (C2 at 8 GPUs: the edge bands are 18 % of the first launch's rows) runs its
+        // edge bands in chains of one cone, at a raised wave priority, and its interior leaves
+        // them their wave slots (overlap_interior): the edges and the exchange behind them are
+        // the block's critical path. A deep slab (C5 at 8 GPUs: 5 %) keeps few long edge chains
+        // and a full-chip interior -- there the short-chain edges took half the chip.
+        if (j == 0) {
+            const int e = r.A.rows() + r.B.rows(), i = r.interior.rows();
+            s->ov_thin = chain_rounds(s->seg_rows(nst)) > 0 && 100 * e >= WS_THIN_PCT * (e + i);
+        }
         // the tuned segment rows (one segment per band -- fewer warm-up rows, longer marches
         // -- measured no faster: the edges are on the critical path at 8 slabs)
-        fused_launch<T>(s, nst, n[j], r.A, r.B, s->seg_rows(nst), s->edge, in, out);
+        const int wgs = fused_launch<T>(s, nst, n[j], r.A, r.B, s->seg_rows(nst), s->edge, in, out, 0,
+                                        s->ov_thin ? WS_EDGE_PRIO : 0, s->ov_thin ? WS_CHAIN_MIN2 : 4);
+        if (j < 8) s->ov_edge_wgs[j] = wgs;
         in = out;
     }
     WS_HIP_CHECK(hipEventRecord(s->ev_edge, s->edge));
@@ -560,7 +575,16 @@ void overlap_interior(ws_sim* s, int steps) {
         ws_grid* out = j + 1 == n.size() ? s->slot[1 - s->cur] : s->ov[j % 2];
         const BandRows r = band_rows(in, C, D);
         s->timer.begin(0, 6.0 * sizeof(T) * g.W * r.interior.rows() * g.L * n[j], s->stream);
-        fused_launch<T>(s, nst, n[j], r.interior, {0, 0}, s->seg_rows(nst), s->stream, in, out);
+        // a chain schedule's interior leaves the wave slots the concurrent edge launch takes:
+        // both launches are then resident together (an interior sized to fill the chip made the
+        // edge bands wait for its waves to drain, and the edges are the block's critical path)
+        const int seg = s->seg_rows(nst);
+        int want = 0;
+        if (s->ov_thin && chain_rounds(seg) > 0 && j < 8 && s->ov_edge_wgs[j] > 0) {
+            const int slots = chain_rounds(seg) * 4 * std::max(1, s->num_cus) / (ws::fused_split(s->kernel) ? 2 : 1);
+            want = std::max(slots / 2, slots - s->ov_edge_wgs[j]);
+        }
+        fused_launch<T>(s, nst, n[j], r.interior, {0, 0}, seg, s->stream, in, out, want);
         s->timer.end(s->stream);
         in = out;
     }
@@ -778,8 +802,8 @@ void run_steps(ws_sim* s, int k) {
     s->metrics.num_steps += k;
 }
 
-template void fused_launch<float>(ws_sim*, int, int, RowRange, RowRange, int, hipStream_t, ws_grid*, ws_grid*);
-template void fused_launch<double>(ws_sim*, int, int, RowRange, RowRange, int, hipStream_t, ws_grid*, ws_grid*);
+template int fused_launch<float>(ws_sim*, int, int, RowRange, RowRange, int, hipStream_t, ws_grid*, ws_grid*, int, int, int);
+template int fused_launch<double>(ws_sim*, int, int, RowRange, RowRange, int, hipStream_t, ws_grid*, ws_grid*, int, int, int);
 template void step_begin<float>(ws_sim*, int);
 template void step_begin<double>(ws_sim*, int);
 template void step_end<float>(ws_sim*, int);

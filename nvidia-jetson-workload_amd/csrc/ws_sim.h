@@ -214,6 +214,8 @@ struct ws_sim {
     hipStream_t edge = nullptr;
     hipEvent_t ev_edge = nullptr, ev_join = nullptr;
     ws_grid* ov[4] = {};      // interior ping-pong (0, 1), edge-band ping-pong (2, 3); u, v, h
+    int ov_edge_wgs[8] = {};  // workgroups of the current block's edge launches (launch j)
+    bool ov_thin = false;     // the block's edge bands are a large share of its rows (overlap_edges)
     double emu_xfer_us = -1.0;  // measurement slab (ws_sim_create_slab_emulated): transfer stand-in
     // slab decomposition
     ws::SlabComm* comm = nullptr;
@@ -223,7 +225,7 @@ struct ws_sim {
     int32_t row0 = 0;
     // chain-schedule tables (ws_schedule.cpp chain_table), one per launch shape, on the device
     struct ChainTable {
-        int64_t key[10];
+        int64_t key[12];
         ws::ChainSeg* dev = nullptr;
         int32_t n = 0, max_rows = 0;
     };
@@ -273,8 +275,10 @@ struct RowRange {
 // the fused step kernel over the output rows A U B (segments of seg_rows rows); in / out
 // default to the current / next grid
 template <typename T>
-void fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st = nullptr,
-                  ws_grid* in = nullptr, ws_grid* out = nullptr);
+// want > 0: a chain schedule's chain count (default: its rounds x the chip's wave slots); returns
+// the workgroups launched
+int fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg_rows, hipStream_t st = nullptr,
+                 ws_grid* in = nullptr, ws_grid* out = nullptr, int want = 0, int prio = 0, int min2 = 4);
 template <typename T>
 void step_begin(ws_sim* s, int nsteps = 1);
 template <typename T>

@@ -59,7 +59,8 @@ for n in [int(x) for x in args.ranks.split(",")]:
                     sim.run(args.steps)
                     dt = (time.perf_counter() - t0) / args.steps
                     best = dt if best is None else min(best, dt)
-                line.append(f"overlap={int(on)} {best * 1e3:.4f}")
+                kern, seg, _ = sim.fused_variant()
+                line.append(f"overlap={int(on)} {best * 1e3:.4f} [{kern} tb={sim.steps_per_launch()} seg={seg}]")
                 del sim
             print(f"ranks={n} rank={rank} block={block} xfer={us:.0f}us/exchange ms/step: " + ", ".join(line),
                   flush=True)
