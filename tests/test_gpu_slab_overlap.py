@@ -227,3 +227,28 @@ def test_fast_numerics_slabs_match_single_domain(nslabs, overlap, monkeypatch):
         assert group.run(n) == n
         one.run(n)
     _check(one, group)
+
+
+@pytest.mark.parametrize("kernel,seg", [("dppy", "-3"), ("dppy", "-2"), ("x2y", "-3"), ("pc", "-3")])
+@pytest.mark.parametrize("H,nslabs", [(8 * 48 + 3, 8), (4 * 130, 4), (2 * 1100, 2)])
+def test_overlap_chain_schedule_thin_and_deep_slabs(H, nslabs, kernel, seg, monkeypatch):
+    """The overlap schedule with the chain schedule pinned (ws_schedule.cpp overlap_edges /
+    overlap_interior): slabs whose edge bands are a large share of their rows (48, 130 rows:
+    the thin-slab path -- one-cone edge chains at raised priority, an interior launch sized to
+    leave them their wave slots) and a deep one (1100 rows: the plain path) == one domain,
+    fp64 RK4 (fast and exact numerics), runs of 13 and 5 steps."""
+    monkeypatch.setenv("WS_KERNEL", kernel)
+    monkeypatch.setenv("WS_TB", "2")
+    monkeypatch.setenv("WS_SEG_ROWS", seg)
+    for numerics in ("fast", "exact"):
+        monkeypatch.setenv("WS_NUMERICS", numerics)
+        def cfg():
+            c = _cfg(300, H, 2, True)
+            c.dy = 1.0  # isotropic spacing: the fast numerics apply
+            return c
+        one, group = _pair(cfg, nslabs, ws.JetStreamInitialCondition())
+        group.set_slab_schedule(6, "on")
+        for n in (13, 5):
+            assert group.run(n) == n
+            one.run(n)
+        _check(one, group)
