@@ -46,6 +46,9 @@ struct FusedArgs {
     // wave issue priority of the launch (s_setprio; 0 = normal): an overlapped slab block's
     // edge bands run beside its interior on the same SIMDs and are the block's critical path
     int32_t prio;
+    // output stores cached (1) or nontemporal (0): a launch whose output fits the Infinity Cache
+    // (the next launch reads it back from there) stores cached (ws_schedule.cpp fused_launch)
+    int32_t cached;
 };
 
 // Spacing / numerics modes of the fused kernels (a template parameter, chosen per launch).

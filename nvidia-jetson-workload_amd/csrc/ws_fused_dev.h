@@ -30,7 +30,7 @@ __device__ __forceinline__ V buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
     else
         return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
 }
-template <typename V>
+template <typename V, int POL = kNT>
 __device__ __forceinline__ void buf_store_nt(V v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     // 16-byte stores take the row offset in voffset, soffset = 0: a dwordx4 store's data
     // VGPRs rewritten by the next VALU instruction need one wait state, and the compiler only
@@ -39,11 +39,11 @@ __device__ __forceinline__ void buf_store_nt(V v, __amdgpu_buffer_rsrc_t r, uint
     // the pair's first element (found on gfx950 at large grids). kDropped + soff stays past
     // every range (soff < 2^31), so dropped stores stay dropped.
     if constexpr (sizeof(V) == 16)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)(voff + soff), 0, kNT);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)(voff + soff), 0, POL);
     else if constexpr (sizeof(V) == 8)
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, kNT);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)voff, (int)soff, POL);
     else
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, kNT);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, POL);
 }
 
 // LDS-DMA: 16 bytes per lane from the buffer into LDS at lds + 16 * lane (wave-uniform base;

@@ -296,9 +296,16 @@ __global__ __launch_bounds__(SPLIT ? 2 * kWave : kWave, SPLIT ? pc_min_waves(CPL
         const bool row_ok = j >= y0 && j < y1;
         const uint32_t so = row_ok ? (uint32_t)(j - y0) * row_bytes : 0u;
         const uint32_t vo = row_ok ? soff : kDropped;
-        buf_store_nt<VT>(o.u, wu, vo, so);
-        buf_store_nt<VT>(o.v, wv, vo, so);
-        buf_store_nt<VT>(o.h, wh, vo, so);
+        // (a.cached is a kernel argument: wave-uniform, both arms issue the same three stores)
+        if (a.cached) {
+            buf_store_nt<VT, 0>(o.u, wu, vo, so);
+            buf_store_nt<VT, 0>(o.v, wv, vo, so);
+            buf_store_nt<VT, 0>(o.h, wh, vo, so);
+        } else {
+            buf_store_nt<VT>(o.u, wu, vo, so);
+            buf_store_nt<VT>(o.v, wv, vo, so);
+            buf_store_nt<VT>(o.h, wh, vo, so);
+        }
     };
 
     // LDS-DMA ring: ring[field][slot][lane], slot = (row - R0) % kNR; one DMA fills kG

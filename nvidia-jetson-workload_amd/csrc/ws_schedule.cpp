@@ -230,6 +230,11 @@ int fused_launch(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int seg
     a.out_w = s->out_w(nst * nsteps);
     a.seg_rows = seg_rows;
     a.prio = prio;
+    {
+        const ws::Geom og = n->geom();
+        const double out_mb = 3.0 * sizeof(T) * og.W * ((double)og.H + 2 * og.halo) * og.L / 1e6;
+        a.cached = (WS_CACHED_PREC >> (sizeof(T) == 8 ? 1 : 0) & 1) && out_mb <= WS_CACHED_MAX_MB ? 1 : 0;
+    }
     a.ga_y0 = A.y0; a.ga_y1 = A.y1; a.ga_n = nA;
     a.gb_y0 = B.y0; a.gb_y1 = B.y1;
     a.seg_n = nA + nB;
