@@ -80,7 +80,13 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
 // cone the y-clamped march (kYClampCost), so those get fewer rows. Chains of neighbouring strips
 // at the same rows are adjacent in the table: xcd_work_item() puts them on one XCD (shared halo
 // columns in its L2). Built on first use per launch shape and kept on the device.
-constexpr double kXClampCost = 1.73, kYClampCost = 1.34;
+#ifndef WS_XCLAMP_COST
+#define WS_XCLAMP_COST 2.5
+#endif
+#ifndef WS_YCLAMP_COST
+#define WS_YCLAMP_COST 1.7
+#endif
+constexpr double kXClampCost = WS_XCLAMP_COST, kYClampCost = WS_YCLAMP_COST;
 
 template <typename T>
 static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
