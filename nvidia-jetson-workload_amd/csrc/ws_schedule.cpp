@@ -80,13 +80,18 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
 // cone the y-clamped march (kYClampCost), so those get fewer rows. Chains of neighbouring strips
 // at the same rows are adjacent in the table: xcd_work_item() puts them on one XCD (shared halo
 // columns in its L2). Built on first use per launch shape and kept on the device.
+// Timed, not counted (round 6, profiles/r06_ab_clamp_cost_*.txt): the fp64 one-column march's
+// clamped bodies cost 3.0 / 2.0 x (C2 RK4 0.1146-0.1157 -> 0.1085-0.1089 ms/step against the
+// instruction-count weights 1.73 / 1.34); the fp32 pair march (C3) keeps 1.73 / 1.34, which it
+// runs fastest with (0.0131-0.0132 against 0.0135-0.0137 at 3.0 / 2.0).
 #ifndef WS_XCLAMP_COST
-#define WS_XCLAMP_COST 2.5
+#define WS_XCLAMP_COST 3.0
 #endif
 #ifndef WS_YCLAMP_COST
-#define WS_YCLAMP_COST 1.7
+#define WS_YCLAMP_COST 2.0
 #endif
-constexpr double kXClampCost = WS_XCLAMP_COST, kYClampCost = WS_YCLAMP_COST;
+constexpr double kXClampCost64 = WS_XCLAMP_COST, kYClampCost64 = WS_YCLAMP_COST;
+constexpr double kXClampCostDef = 1.73, kYClampCostDef = 1.34;
 
 template <typename T>
 static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
@@ -107,6 +112,9 @@ static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, Row
     const int64_t want = want_chains > 0 ? want_chains : (int64_t)rounds * 4 * std::max(1, s->num_cus) / waves_per_wg;
     const int cone = nst * nsteps;
     const int nstrips = (int)ws::fused_strips(s->kernel, g->W, cone, (int)elem_size(s->dtype), out_w);
+    const bool col64 = s->dtype == WS_F64 && !ws::fused_pairs(s->kernel);
+    const double kXClampCost = col64 ? kXClampCost64 : kXClampCostDef;
+    const double kYClampCost = col64 ? kYClampCost64 : kYClampCostDef;
     struct Group {
         int unit;
         RowRange r;
