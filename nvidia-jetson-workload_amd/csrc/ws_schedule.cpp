@@ -91,7 +91,13 @@ static RowRange step_rows(const ws_sim* s, int nst, int nsteps) {
 #define WS_YCLAMP_COST 2.0
 #endif
 constexpr double kXClampCost64 = WS_XCLAMP_COST, kYClampCost64 = WS_YCLAMP_COST;
-constexpr double kXClampCostDef = 1.73, kYClampCostDef = 1.34;
+#ifndef WS_XCLAMP_COST_DEF
+#define WS_XCLAMP_COST_DEF 1.73
+#endif
+#ifndef WS_YCLAMP_COST_DEF
+#define WS_YCLAMP_COST_DEF 1.34
+#endif
+constexpr double kXClampCostDef = WS_XCLAMP_COST_DEF, kYClampCostDef = WS_YCLAMP_COST_DEF;
 
 template <typename T>
 static const ws_sim::ChainTable& chain_table(ws_sim* s, int nst, int nsteps, RowRange A, RowRange B, int rounds,
